@@ -1,0 +1,78 @@
+/*
+ * enet_oracle.h -- CPU restatement of the EphemeralNet crypto hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (ephemeralnet_amd/, the
+ * C-ABI library, the C++ API) links, loads or calls this code.  It is imported
+ * only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+ * always as the checker / CPU baseline, never as the thing measured.
+ *
+ * Parity is pinned against the JSON fixtures in tests/golden/, which were generated from the
+ * reference src/crypto compiled in the survey container (oracle/_ref, see
+ * oracle/Makefile) and, for Poly1305 / AEAD (absent from the reference), from
+ * OpenSSL 3.0.2 plus the RFC 8439 vectors (tests/golden/gen_golden.py).
+ *
+ * Each function cites the reference file:line it restates.  Paths are relative
+ * to the reference tree (ShardianLabs/EphemeralNet @ 2025-11-28).
+ */
+#ifndef ENET_ORACLE_H
+#define ENET_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* splitmix64 byte generator shared by fixtures, tests and bench:
+ * byte stream = concat_i LE64(mix(seed + (i+1) * 0x9E3779B97F4A7C15)). */
+void orc_splitmix_bytes(uint64_t seed, uint8_t* out, size_t n);
+
+/* src/crypto/ChaCha20.cpp:56-94 (chacha20_block) */
+void orc_chacha20_block(const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                        uint8_t out[64]);
+/* src/crypto/ChaCha20.cpp:98-121 (ChaCha20::apply): byte-wise XOR, u32 counter wrap */
+void orc_chacha20_xor(const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                      const uint8_t* in, uint8_t* out, size_t n);
+
+/* src/crypto/Sha256.cpp:66-176 (Sha256::digest) */
+void orc_sha256(const uint8_t* data, size_t n, uint8_t out[32]);
+/* src/crypto/HmacSha256.cpp:11-39 (HmacSha256::compute) */
+void orc_hmac_sha256(const uint8_t* key, size_t klen, const uint8_t* data, size_t n,
+                     uint8_t out[32]);
+/* src/crypto/HmacSha256.cpp:41-54 (HmacSha256::verify) */
+int orc_hmac_sha256_verify(const uint8_t* key, size_t klen, const uint8_t* data, size_t n,
+                           const uint8_t* mac, size_t maclen);
+
+/* RFC 8439 section 2.5 Poly1305 (no reference implementation exists) */
+void orc_poly1305(const uint8_t key[32], const uint8_t* msg, size_t n, uint8_t tag[16]);
+/* RFC 8439 section 2.8 AEAD_CHACHA20_POLY1305 */
+void orc_aead_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* aad,
+                   size_t aad_len, const uint8_t* pt, size_t n, uint8_t* ct, uint8_t tag[16]);
+int orc_aead_open(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* aad,
+                  size_t aad_len, const uint8_t* ct, size_t n, const uint8_t tag[16],
+                  uint8_t* pt);
+
+/* src/crypto/CryptoManager.cpp:8-13 (derive_counter): LE32(chunk_id[0..3]) */
+uint32_t orc_derive_counter(const uint8_t chunk_id[32]);
+
+/* Session frame body, src/protocol/Message.cpp:305-311 + src/network/SessionManager.cpp:362-374:
+ *   body = ChaCha20_{K,N,ctr=0}(m || HMAC-SHA256_K(m)),  |body| = n + 32.
+ * The wire frame is nonce(12) || BE32(n+32) || body (SessionManager.cpp:376-387). */
+void orc_frame_seal(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* m, size_t n,
+                    uint8_t* body);
+/* Inverse: SessionManager.cpp:815-822 then Message.cpp:313-328.  body_len >= 32 or fails. */
+int orc_frame_open(const uint8_t key[32], const uint8_t nonce[12], const uint8_t* body,
+                   size_t body_len, uint8_t* m_out);
+
+/* CPU baseline: AEAD seal then open over n records of len bytes (record i uses key
+ * keys+32*i, nonce nonces+12*i), split over `threads` std::threads-equivalent pthreads.
+ * Returns seconds for seal (out[0]) and open (out[1]); returns number of failed opens. */
+int orc_bench_aead(const uint8_t* pt, uint8_t* ct, uint8_t* back, const uint8_t* keys,
+                   const uint8_t* nonces, uint8_t* tags, size_t n, size_t len, int threads,
+                   double out_seconds[2]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

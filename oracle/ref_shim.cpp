@@ -1,0 +1,118 @@
+// ref_shim.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A C-linkage veneer over the *reference* src/crypto and src/protocol/Message.cpp, compiled
+// from the sources where they lie under /root/reference (see oracle/Makefile; output goes to
+// oracle/_ref/, which is git-ignored).  It exists so tests/golden/gen_golden.py can generate
+// golden vectors from the reference itself, and so the restatement in enet_oracle.c can be
+// validated against it.  No reference source is copied into this repository.
+#include "ephemeralnet/crypto/ChaCha20.hpp"
+#include "ephemeralnet/crypto/CryptoManager.hpp"
+#include "ephemeralnet/crypto/HmacSha256.hpp"
+#include "ephemeralnet/crypto/Sha256.hpp"
+#include "ephemeralnet/protocol/Message.hpp"
+
+#include <algorithm>
+#include <cstring>
+
+using namespace ephemeralnet;
+
+extern "C" {
+
+// ChaCha20::apply (src/crypto/ChaCha20.cpp:98-121)
+void ref_chacha20_apply(const uint8_t* key, const uint8_t* nonce, const uint8_t* in, size_t n,
+                        uint8_t* out, uint32_t counter) {
+    crypto::Key k{};
+    crypto::Nonce nn{};
+    std::memcpy(k.bytes.data(), key, 32);
+    std::memcpy(nn.bytes.data(), nonce, 12);
+    std::vector<uint8_t> o;
+    crypto::ChaCha20::apply(k, nn, std::span<const uint8_t>(in, n), o, counter);
+    if (n) std::memcpy(out, o.data(), n);
+}
+
+// Sha256::digest (src/crypto/Sha256.cpp:128-132)
+void ref_sha256(const uint8_t* data, size_t n, uint8_t* out) {
+    auto d = crypto::Sha256::digest(std::span<const uint8_t>(data, n));
+    std::memcpy(out, d.data(), 32);
+}
+
+// Sha256 streaming update()/finalize() with a fixed piece size (Sha256.cpp:72-126)
+void ref_sha256_pieces(const uint8_t* data, size_t n, size_t piece, uint8_t* out) {
+    crypto::Sha256 h;
+    for (size_t o = 0; o < n; o += piece) h.update(std::span<const uint8_t>(data + o, std::min(piece, n - o)));
+    auto d = h.finalize();
+    std::memcpy(out, d.data(), 32);
+}
+
+// HmacSha256::compute / verify (src/crypto/HmacSha256.cpp:11-54)
+void ref_hmac(const uint8_t* key, size_t klen, const uint8_t* data, size_t n, uint8_t* out) {
+    auto d = crypto::HmacSha256::compute(std::span<const uint8_t>(key, klen), std::span<const uint8_t>(data, n));
+    std::memcpy(out, d.data(), 32);
+}
+int ref_hmac_verify(const uint8_t* key, size_t klen, const uint8_t* data, size_t n, const uint8_t* mac,
+                    size_t maclen) {
+    return crypto::HmacSha256::verify(std::span<const uint8_t>(key, klen), std::span<const uint8_t>(data, n),
+                                      std::span<const uint8_t>(mac, maclen))
+               ? 1
+               : 0;
+}
+
+// CryptoManager::encrypt_with_key / decrypt_with_key (src/crypto/CryptoManager.cpp:77-90).
+// The nonce is drawn by the reference's own mt19937_64; it is returned so callers can check.
+void ref_cm_encrypt_with_key(const uint8_t* key, const uint8_t* chunk_id, const uint8_t* pt, size_t n,
+                             uint8_t* ct, uint8_t* nonce_out) {
+    crypto::Key k{};
+    std::memcpy(k.bytes.data(), key, 32);
+    ChunkId id{};
+    std::memcpy(id.data(), chunk_id, 32);
+    ChunkData p(pt, pt + n);
+    auto c = crypto::CryptoManager::encrypt_with_key(k, id, p);
+    if (n) std::memcpy(ct, c.data.data(), n);
+    std::memcpy(nonce_out, c.nonce.bytes.data(), 12);
+}
+void ref_cm_decrypt_with_key(const uint8_t* key, const uint8_t* chunk_id, const uint8_t* ct, size_t n,
+                             const uint8_t* nonce, uint8_t* pt) {
+    crypto::Key k{};
+    std::memcpy(k.bytes.data(), key, 32);
+    ChunkId id{};
+    std::memcpy(id.data(), chunk_id, 32);
+    crypto::Nonce nn{};
+    std::memcpy(nn.bytes.data(), nonce, 12);
+    auto p = crypto::CryptoManager::decrypt_with_key(k, id, std::span<const uint8_t>(ct, n), nn);
+    if (n) std::memcpy(pt, p->data(), n);
+}
+
+// protocol::encode_signed (src/protocol/Message.cpp:305-311) for a Request and a Chunk message.
+size_t ref_encode_signed_request(const uint8_t* chunk_id, const uint8_t* requester, const uint8_t* key,
+                                 size_t klen, uint8_t* out, size_t cap) {
+    protocol::Message m{};
+    m.type = protocol::MessageType::Request;
+    protocol::RequestPayload p{};
+    std::memcpy(p.chunk_id.data(), chunk_id, 32);
+    std::memcpy(p.requester.data(), requester, 32);
+    m.payload = p;
+    auto v = protocol::encode_signed(m, std::span<const uint8_t>(key, klen));
+    if (v.size() <= cap) std::memcpy(out, v.data(), v.size());
+    return v.size();
+}
+size_t ref_encode_signed_chunk(const uint8_t* chunk_id, const uint8_t* data, size_t n, int64_t ttl,
+                               const uint8_t* key, size_t klen, uint8_t* out, size_t cap) {
+    protocol::Message m{};
+    m.type = protocol::MessageType::Chunk;
+    protocol::ChunkPayload p{};
+    std::memcpy(p.chunk_id.data(), chunk_id, 32);
+    p.data.assign(data, data + n);
+    p.ttl = std::chrono::seconds(ttl);
+    m.payload = p;
+    auto v = protocol::encode_signed(m, std::span<const uint8_t>(key, klen));
+    if (v.size() <= cap) std::memcpy(out, v.data(), v.size());
+    return v.size();
+}
+// protocol::decode_signed (Message.cpp:313-328): 1 when it yields a message.
+int ref_decode_signed_ok(const uint8_t* buf, size_t n, const uint8_t* key, size_t klen) {
+    return protocol::decode_signed(std::span<const uint8_t>(buf, n), std::span<const uint8_t>(key, klen)).has_value()
+               ? 1
+               : 0;
+}
+
+}  // extern "C"
