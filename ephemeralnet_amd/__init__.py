@@ -1,0 +1,234 @@
+"""ephemeralnet_amd -- MI355X bulk crypto engine for EphemeralNet's data path.
+
+Python view of libenet_crypto.so's C ABI (include/enet_crypto.h) over torch device tensors
+(torch is plumbing here: device memory and streams).  The product path is the HIP library:
+there is no CPU fallback, and importing the package without the built library raises.
+
+Operations mirror the reference src/crypto API, batched (ShardianLabs/EphemeralNet):
+  chacha20_xor   ChaCha20::apply            src/crypto/ChaCha20.cpp:98-121
+  aead_seal/open RFC 8439 (README.md:49 promise; no reference implementation)
+  sha256         Sha256::digest             src/crypto/Sha256.cpp:128-132
+  hmac_sha256    HmacSha256::compute/verify src/crypto/HmacSha256.cpp:11-54
+  frame_seal/open encode_signed + SessionManager frame body
+                  src/protocol/Message.cpp:305-328, src/network/SessionManager.cpp:362-374,815-822
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libenet_crypto.so")
+
+ENET_OK = 0
+
+
+class EnetError(RuntimeError):
+    pass
+
+
+class _Records(C.Structure):
+    _fields_ = [
+        ("count", C.c_uint32),
+        ("in_offsets", C.c_void_p),
+        ("out_offsets", C.c_void_p),
+        ("in_", C.c_void_p),
+        ("out", C.c_void_p),
+        ("keys", C.c_void_p),
+        ("key_stride", C.c_uint32),
+        ("nonces", C.c_void_p),
+        ("order", C.c_void_p),
+        ("total_bytes_hint", C.c_uint64),
+        ("max_len_hint", C.c_uint32),
+    ]
+
+
+EXPORTS = [
+    "enet_chacha20_xor_batch", "enet_aead_seal_batch", "enet_aead_open_batch",
+    "enet_sha256_batch", "enet_hmac_sha256_batch", "enet_hmac_sha256_verify_batch",
+    "enet_frame_seal_batch", "enet_frame_open_batch", "enet_chunk_counter",
+    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_last_error", "enet_abi_version",
+]
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """Load the in-tree HIP library (fails loudly when it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EnetError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
+                            "g.build()'` (hipcc --offload-arch=gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        rp = C.POINTER(_Records)
+        L.enet_chacha20_xor_batch.argtypes = [rp, vp, vp]
+        L.enet_aead_seal_batch.argtypes = [rp, vp, vp, vp, vp]
+        L.enet_aead_open_batch.argtypes = [rp, vp, vp, vp, vp, vp]
+        L.enet_sha256_batch.argtypes = [u32, vp, vp, vp, vp]
+        L.enet_hmac_sha256_batch.argtypes = [u32, vp, vp, u32, vp, vp, vp, vp]
+        L.enet_hmac_sha256_verify_batch.argtypes = [u32, vp, vp, u32, vp, vp, vp, vp, vp]
+        L.enet_frame_seal_batch.argtypes = [rp, vp]
+        L.enet_frame_open_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_chunk_counter.argtypes = [C.c_char_p]
+        L.enet_chunk_counter.restype = u32
+        L.enet_lanes_per_record.argtypes = [u32, u64, u32]
+        L.enet_lanes_per_record.restype = u32
+        L.enet_set_lanes_per_record.argtypes = [u32]
+        L.enet_last_error.restype = C.c_char_p
+        L.enet_abi_version.restype = u32
+        for name in EXPORTS:
+            getattr(L, name)
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != ENET_OK:
+        msg = lib().enet_last_error().decode(errors="replace")
+        raise EnetError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+@dataclass
+class Batch:
+    """Device-resident SoA record batch (all torch tensors on the GPU).
+
+    arena: uint8 [total]; offsets: int64 [n+1]; keys: uint8 [n,32] (or [1,32] with
+    key_stride=0); nonces: uint8 [n,12].  `out`/`out_offsets` default to a same-shape arena.
+    """
+    arena: "object"
+    offsets: "object"
+    keys: "object"
+    nonces: "object"
+    key_stride: int = 32
+    order: "object" = None
+    total_bytes_hint: int = 0
+    max_len_hint: int = 0
+
+    @property
+    def n(self) -> int:
+        return int(self.offsets.numel()) - 1
+
+    def records(self, out, out_offsets) -> _Records:
+        r = _Records()
+        r.count = self.n
+        r.in_offsets = _ptr(self.offsets)
+        r.out_offsets = _ptr(out_offsets)
+        r.in_ = _ptr(self.arena)
+        r.out = _ptr(out)
+        r.keys = _ptr(self.keys)
+        r.key_stride = self.key_stride
+        r.nonces = _ptr(self.nonces)
+        r.order = _ptr(self.order)
+        r.total_bytes_hint = self.total_bytes_hint
+        r.max_len_hint = self.max_len_hint
+        return r
+
+
+def chacha20_xor(b: Batch, out, counters=None, out_offsets=None, stream=None) -> None:
+    r = b.records(out, b.offsets if out_offsets is None else out_offsets)
+    _check(lib().enet_chacha20_xor_batch(C.byref(r), _ptr(counters), _stream(stream)),
+           "enet_chacha20_xor_batch")
+
+
+def aead_seal(b: Batch, out, tags, aad=None, aad_offsets=None, stream=None) -> None:
+    r = b.records(out, b.offsets)
+    _check(lib().enet_aead_seal_batch(C.byref(r), _ptr(aad), _ptr(aad_offsets), _ptr(tags),
+                                      _stream(stream)), "enet_aead_seal_batch")
+
+
+def aead_open(b: Batch, out, tags, ok, aad=None, aad_offsets=None, stream=None) -> None:
+    r = b.records(out, b.offsets)
+    _check(lib().enet_aead_open_batch(C.byref(r), _ptr(aad), _ptr(aad_offsets), _ptr(tags),
+                                      _ptr(ok), _stream(stream)), "enet_aead_open_batch")
+
+
+def sha256(arena, offsets, digests, stream=None) -> None:
+    n = int(offsets.numel()) - 1
+    _check(lib().enet_sha256_batch(n, _ptr(arena), _ptr(offsets), _ptr(digests), _stream(stream)),
+           "enet_sha256_batch")
+
+
+def hmac_sha256(keys, arena, offsets, macs, key_offsets=None, key_stride=32, stream=None) -> None:
+    n = int(offsets.numel()) - 1
+    _check(lib().enet_hmac_sha256_batch(n, _ptr(keys), _ptr(key_offsets), key_stride, _ptr(arena),
+                                        _ptr(offsets), _ptr(macs), _stream(stream)),
+           "enet_hmac_sha256_batch")
+
+
+def hmac_sha256_verify(keys, arena, offsets, macs, ok, key_offsets=None, key_stride=32,
+                       stream=None) -> None:
+    n = int(offsets.numel()) - 1
+    _check(lib().enet_hmac_sha256_verify_batch(n, _ptr(keys), _ptr(key_offsets), key_stride,
+                                               _ptr(arena), _ptr(offsets), _ptr(macs), _ptr(ok),
+                                               _stream(stream)), "enet_hmac_sha256_verify_batch")
+
+
+def frame_seal(b: Batch, out, out_offsets, stream=None) -> None:
+    r = b.records(out, out_offsets)
+    _check(lib().enet_frame_seal_batch(C.byref(r), _stream(stream)), "enet_frame_seal_batch")
+
+
+def frame_open(b: Batch, out, out_offsets, macs, ok, stream=None) -> None:
+    r = b.records(out, out_offsets)
+    _check(lib().enet_frame_open_batch(C.byref(r), _ptr(macs), _ptr(ok), _stream(stream)),
+           "enet_frame_open_batch")
+
+
+def chunk_counter(chunk_id: bytes) -> int:
+    """LE32(chunk_id[0..3]) -- CryptoManager.cpp:8-13."""
+    return int(lib().enet_chunk_counter(chunk_id))
+
+
+def lanes_per_record(count: int, total_bytes: int = 0, max_len: int = 0) -> int:
+    return int(lib().enet_lanes_per_record(count, total_bytes, max_len))
+
+
+def set_lanes_per_record(lanes: int) -> None:
+    """Force lanes per record (1/2/4/8/16); 0 restores the scheduler."""
+    _check(lib().enet_set_lanes_per_record(lanes), "enet_set_lanes_per_record")
+
+
+def make_batch(items: Sequence[bytes], keys: Sequence[bytes], nonces: Sequence[bytes],
+               device="cuda", key_stride: int = 32, base_offset: int = 0) -> Batch:
+    """Pack host byte strings into a device Batch.  `base_offset` shifts every record start
+    (e.g. 3 -> unaligned starts) by leaving a gap at the front of the arena."""
+    import numpy as np
+    import torch
+    offs = [base_offset]
+    for it in items:
+        offs.append(offs[-1] + len(it))
+    total = offs[-1]
+    buf = np.zeros(max(total, 1), dtype=np.uint8)
+    for i, it in enumerate(items):
+        if it:
+            buf[offs[i]:offs[i] + len(it)] = np.frombuffer(it, dtype=np.uint8)
+    kb = b"".join(keys)
+    nb = b"".join(nonces)
+    return Batch(
+        arena=torch.from_numpy(buf).to(device),
+        offsets=torch.tensor(offs, dtype=torch.int64, device=device),
+        keys=torch.frombuffer(bytearray(kb), dtype=torch.uint8).to(device),
+        nonces=torch.frombuffer(bytearray(nb), dtype=torch.uint8).to(device),
+        key_stride=key_stride,
+        total_bytes_hint=total - base_offset,
+        max_len_hint=max((len(i) for i in items), default=0),
+    )

@@ -1,0 +1,260 @@
+// capi.cpp -- the extern "C" boundary (include/enet_crypto.h): argument checks, lane
+// scheduling, and the kernel sequences for the composite operations (frames).
+#include "enet_crypto.h"
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "enet_internal.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* what) {
+    g_last_error = what;
+    return code;
+}
+
+int hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) {
+        g_last_error.clear();
+        return ENET_OK;
+    }
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return ENET_EHIP;
+}
+
+bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
+
+int check_records(const enet_records* r, bool need_keys) {
+    if (!r) return fail(ENET_EINVAL, "records descriptor is NULL");
+    if (r->count == 0) return ENET_OK;
+    if (!r->in_offsets || !r->out_offsets || !r->in || !r->out)
+        return fail(ENET_EINVAL, "records: NULL offsets or arena");
+    if (need_keys) {
+        if (!r->keys || !r->nonces) return fail(ENET_EINVAL, "records: NULL keys or nonces");
+        if (r->key_stride != 0 && r->key_stride != 32)
+            return fail(ENET_EINVAL, "records: key_stride must be 0 or 32");
+        if (!aligned4(r->keys) || !aligned4(r->nonces))
+            return fail(ENET_EINVAL, "records: keys/nonces must be 4-byte aligned");
+    }
+    if (r->order && !aligned4(r->order)) return fail(ENET_EINVAL, "records: order misaligned");
+    return ENET_OK;
+}
+
+enet::RecParams rec_params(const enet_records* r) {
+    enet::RecParams p{};
+    p.n = r->count;
+    p.in_off = r->in_offsets;
+    p.out_off = r->out_offsets;
+    p.in = r->in;
+    p.out = r->out;
+    p.keys = r->keys;
+    p.key_stride = r->key_stride;
+    p.nonces = r->nonces;
+    p.order = r->order;
+    return p;
+}
+
+uint32_t lanes_for(const enet_records* r) {
+    return enet::choose_lanes(r->count, r->total_bytes_hint, r->max_len_hint);
+}
+
+}  // namespace
+
+namespace enet {
+
+static std::atomic<uint32_t> g_forced_lanes{0};
+
+// Give each record enough lanes that the grid holds >= ENET_TARGET_LANES lanes
+// (default 2 waves per SIMD on 256 CUs = 131072) without giving a record more lanes than it
+// has 64-byte blocks.  ENET_LANES forces a value (tuning / tests).
+uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len) {
+    static const uint32_t forced = [] {
+        const char* s = std::getenv("ENET_LANES");
+        return s ? (uint32_t)std::strtoul(s, nullptr, 10) : 0u;
+    }();
+    static const uint64_t target = [] {
+        const char* s = std::getenv("ENET_TARGET_LANES");
+        return s ? (uint64_t)std::strtoull(s, nullptr, 10) : 131072ull;
+    }();
+    if (uint32_t f = g_forced_lanes.load(std::memory_order_relaxed)) return f;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16) return forced;
+    if (n == 0) return 1;
+    uint64_t blocks_cap = kMaxLanesPerRecord;
+    uint64_t typical = max_len ? max_len : (total_bytes ? total_bytes / n : 0);
+    if (typical) blocks_cap = (typical + 63) / 64;
+    uint32_t lanes = 1;
+    while (lanes < kMaxLanesPerRecord && (uint64_t)n * lanes < target && lanes * 2 <= blocks_cap)
+        lanes *= 2;
+    return lanes;
+}
+
+}  // namespace enet
+
+extern "C" {
+
+uint32_t enet_abi_version(void) { return (1u << 16) | 0u; }
+
+const char* enet_last_error(void) { return g_last_error.c_str(); }
+
+uint32_t enet_chunk_counter(const uint8_t chunk_id[32]) {  // CryptoManager.cpp:8-13
+    return (uint32_t)chunk_id[0] | ((uint32_t)chunk_id[1] << 8) | ((uint32_t)chunk_id[2] << 16) |
+           ((uint32_t)chunk_id[3] << 24);
+}
+
+uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t max_len) {
+    return enet::choose_lanes(count, total_bytes, max_len);
+}
+
+int enet_set_lanes_per_record(uint32_t lanes) {
+    if (lanes != 0 && lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16)
+        return fail(ENET_EINVAL, "lanes must be 0, 1, 2, 4, 8 or 16");
+    enet::g_forced_lanes.store(lanes, std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+int enet_chacha20_xor_batch(const enet_records* r, const uint32_t* counters, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (counters && !aligned4(counters)) return fail(ENET_EINVAL, "counters misaligned");
+    enet::RecParams p = rec_params(r);
+    p.counters = counters;
+    return hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), (hipStream_t)stream),
+                      "chacha20_xor launch");
+}
+
+int enet_aead_seal_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
+                         uint8_t* tags, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!tags || !aligned4(tags)) return fail(ENET_EINVAL, "tags NULL or misaligned");
+    if ((aad == nullptr) != (aad_offsets == nullptr))
+        return fail(ENET_EINVAL, "aad and aad_offsets must both be set or both NULL");
+    enet::RecParams p = rec_params(r);
+    p.aad = aad;
+    p.aad_off = aad_offsets;
+    p.tag_out = tags;
+    return hip_status(enet::launch_records(enet::MODE_SEAL, p, lanes_for(r), (hipStream_t)stream),
+                      "aead_seal launch");
+}
+
+int enet_aead_open_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
+                         const uint8_t* tags, uint8_t* ok, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!tags || !aligned4(tags) || !ok) return fail(ENET_EINVAL, "tags/ok NULL or misaligned");
+    if ((aad == nullptr) != (aad_offsets == nullptr))
+        return fail(ENET_EINVAL, "aad and aad_offsets must both be set or both NULL");
+    enet::RecParams p = rec_params(r);
+    p.aad = aad;
+    p.aad_off = aad_offsets;
+    p.tag_in = tags;
+    p.ok = ok;
+    return hip_status(enet::launch_records(enet::MODE_OPEN, p, lanes_for(r), (hipStream_t)stream),
+                      "aead_open launch");
+}
+
+int enet_sha256_batch(uint32_t n, const uint8_t* in, const uint64_t* offsets, uint8_t* digests,
+                      void* stream) {
+    if (n == 0) return ENET_OK;
+    if (!in || !offsets || !digests) return fail(ENET_EINVAL, "sha256: NULL argument");
+    enet::ShaParams p{};
+    p.n = n;
+    p.in = in;
+    p.off = offsets;
+    p.digest = digests;
+    return hip_status(enet::launch_sha(p, (hipStream_t)stream), "sha256 launch");
+}
+
+static int hmac_common(uint32_t n, const uint8_t* keys, const uint64_t* key_offsets,
+                       uint32_t key_stride, const uint8_t* in, const uint64_t* offsets,
+                       enet::ShaParams& p) {
+    if (!keys || !in || !offsets) return fail(ENET_EINVAL, "hmac: NULL argument");
+    if (!key_offsets && key_stride != 0 && key_stride != 32)
+        return fail(ENET_EINVAL, "hmac: key_stride must be 0 or 32");
+    p.n = n;
+    p.in = in;
+    p.off = offsets;
+    p.keys = keys;
+    p.key_off = key_offsets;
+    p.key_stride = key_stride;
+    return ENET_OK;
+}
+
+int enet_hmac_sha256_batch(uint32_t n, const uint8_t* keys, const uint64_t* key_offsets,
+                           uint32_t key_stride, const uint8_t* in, const uint64_t* offsets,
+                           uint8_t* macs, void* stream) {
+    if (n == 0) return ENET_OK;
+    enet::ShaParams p{};
+    if (int e = hmac_common(n, keys, key_offsets, key_stride, in, offsets, p)) return e;
+    if (!macs) return fail(ENET_EINVAL, "hmac: NULL macs");
+    p.digest = macs;
+    return hip_status(enet::launch_sha(p, (hipStream_t)stream), "hmac launch");
+}
+
+int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, const uint64_t* key_offsets,
+                                  uint32_t key_stride, const uint8_t* in,
+                                  const uint64_t* offsets, const uint8_t* macs, uint8_t* ok,
+                                  void* stream) {
+    if (n == 0) return ENET_OK;
+    enet::ShaParams p{};
+    if (int e = hmac_common(n, keys, key_offsets, key_stride, in, offsets, p)) return e;
+    if (!macs || !ok) return fail(ENET_EINVAL, "hmac verify: NULL macs/ok");
+    p.expect = macs;
+    p.ok = ok;
+    return hip_status(enet::launch_sha(p, (hipStream_t)stream), "hmac verify launch");
+}
+
+int enet_frame_seal_batch(const enet_records* r, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    // 1) MAC = HMAC-SHA256(K, m) written in clear at the tail of each output record
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->in;
+    s.off = r->in_offsets;
+    s.digest = r->out;
+    s.dest_off = r->out_offsets;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.order = r->order;
+    hipStream_t st = (hipStream_t)stream;
+    if (int e = hip_status(enet::launch_sha(s, st), "frame_seal hmac launch")) return e;
+    // 2) body = ChaCha20(ctr 0) over m || MAC
+    enet::RecParams p = rec_params(r);
+    return hip_status(enet::launch_records(3, p, lanes_for(r), st), "frame_seal chacha launch");
+}
+
+int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!macs || !ok) return fail(ENET_EINVAL, "frame_open: NULL macs/ok");
+    hipStream_t st = (hipStream_t)stream;
+    // 1) decrypt: message bytes to out, MAC bytes to macs
+    enet::RecParams p = rec_params(r);
+    p.tag_out = macs;
+    if (int e = hip_status(enet::launch_records(4, p, lanes_for(r), st), "frame_open chacha"))
+        return e;
+    // 2) verify HMAC over the decrypted message; zero the message on failure
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->out;
+    s.off = r->out_offsets;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.expect = macs;
+    s.ok = ok;
+    s.guard_off = r->in_offsets;
+    s.zero_on_fail = r->out;
+    s.order = r->order;
+    return hip_status(enet::launch_sha(s, st), "frame_open hmac verify");
+}
+
+}  // extern "C"

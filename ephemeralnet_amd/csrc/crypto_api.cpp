@@ -1,0 +1,452 @@
+// crypto_api.cpp -- the reference C++ API (namespace ephemeralnet::crypto) implemented on the
+// MI355X through the C ABI.  Every call ships its record(s) to the device, runs the batch
+// kernels and copies the result back; there is no CPU crypto path in the product (a failing
+// GPU path throws std::runtime_error instead of silently computing on the host).
+//
+// Reference: src/crypto/{ChaCha20,Sha256,HmacSha256,CryptoManager}.cpp (ShardianLabs/EphemeralNet).
+#include "ephemeralnet/crypto/Batch.hpp"
+#include "ephemeralnet/crypto/ChaCha20.hpp"
+#include "ephemeralnet/crypto/CryptoManager.hpp"
+#include "ephemeralnet/crypto/HmacSha256.hpp"
+#include "ephemeralnet/crypto/Sha256.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "enet_crypto.h"
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("enet: ") + what + ": " + hipGetErrorString(e));
+}
+
+void enet_check(int rc, const char* what) {
+    if (rc != ENET_OK) throw std::runtime_error(std::string("enet: ") + what + ": " + enet_last_error());
+}
+
+// Grow-only device buffers + one stream per host thread: the reference functions are
+// reentrant and called from many session threads (SessionManager.cpp:332,703).
+struct Staging {
+    static constexpr int kSlots = 10;
+    void* dev[kSlots] = {};
+    size_t cap[kSlots] = {};
+    hipStream_t stream = nullptr;
+
+    ~Staging() {
+        for (int i = 0; i < kSlots; ++i)
+            if (dev[i]) (void)hipFree(dev[i]);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+    void* get(int slot, size_t bytes) {
+        bytes = std::max<size_t>(bytes, 64);
+        if (cap[slot] < bytes) {
+            if (dev[slot]) hip_check(hipFree(dev[slot]), "hipFree");
+            size_t c = std::max(bytes, cap[slot] * 2);
+            hip_check(hipMalloc(&dev[slot], c), "hipMalloc");
+            cap[slot] = c;
+        }
+        return dev[slot];
+    }
+    hipStream_t s() {
+        if (!stream) hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+        return stream;
+    }
+    void h2d(void* d, const void* h, size_t n) {
+        if (n) hip_check(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s()), "H2D");
+    }
+    void d2h(void* h, const void* d, size_t n) {
+        if (n) hip_check(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s()), "D2H");
+    }
+    void sync() { hip_check(hipStreamSynchronize(s()), "hipStreamSynchronize"); }
+};
+
+Staging& staging() {
+    thread_local Staging st;
+    return st;
+}
+
+enum Slot { S_IN = 0, S_OUT, S_INOFF, S_OUTOFF, S_KEYS, S_NONCES, S_CTR, S_TAGS, S_OK, S_AUX };
+
+// Host-side packing of a list of byte spans into one arena + offsets.
+struct Packed {
+    std::vector<uint8_t> arena;
+    std::vector<uint64_t> off;
+};
+
+Packed pack(std::span<const std::span<const uint8_t>> items, size_t extra_per_item = 0) {
+    Packed p;
+    p.off.resize(items.size() + 1);
+    uint64_t total = 0;
+    for (size_t i = 0; i < items.size(); ++i) {
+        p.off[i] = total;
+        total += items[i].size() + extra_per_item;
+    }
+    p.off[items.size()] = total;
+    p.arena.resize(total);
+    for (size_t i = 0; i < items.size(); ++i)
+        if (!items[i].empty()) std::memcpy(p.arena.data() + p.off[i], items[i].data(), items[i].size());
+    return p;
+}
+
+std::vector<uint64_t> offsets_of(std::span<const std::span<const uint8_t>> items, int64_t delta) {
+    std::vector<uint64_t> off(items.size() + 1);
+    uint64_t total = 0;
+    for (size_t i = 0; i < items.size(); ++i) {
+        off[i] = total;
+        int64_t len = (int64_t)items[i].size() + delta;
+        total += (uint64_t)std::max<int64_t>(len, 0);
+    }
+    off[items.size()] = total;
+    return off;
+}
+
+struct DevRecords {
+    enet_records r{};
+    uint8_t* out = nullptr;
+    uint64_t out_total = 0;
+};
+
+// Upload arenas, offsets, keys and nonces; returns the descriptor pointing at device copies.
+DevRecords upload(Staging& st, const Packed& in, const std::vector<uint64_t>& out_off,
+                  const uint8_t* keys, size_t key_bytes, uint32_t key_stride, const uint8_t* nonces,
+                  size_t n) {
+    DevRecords d;
+    auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
+    d.out_total = out_off.back();
+    d.out = (uint8_t*)st.get(S_OUT, d.out_total);
+    auto* dinoff = (uint64_t*)st.get(S_INOFF, in.off.size() * 8);
+    auto* doutoff = (uint64_t*)st.get(S_OUTOFF, out_off.size() * 8);
+    auto* dkeys = (uint8_t*)st.get(S_KEYS, key_bytes);
+    auto* dnon = (uint8_t*)st.get(S_NONCES, 12 * n);
+    st.h2d(din, in.arena.data(), in.arena.size());
+    st.h2d(dinoff, in.off.data(), in.off.size() * 8);
+    st.h2d(doutoff, out_off.data(), out_off.size() * 8);
+    st.h2d(dkeys, keys, key_bytes);
+    st.h2d(dnon, nonces, 12 * n);
+    d.r.count = (uint32_t)n;
+    d.r.in_offsets = dinoff;
+    d.r.out_offsets = doutoff;
+    d.r.in = din;
+    d.r.out = d.out;
+    d.r.keys = dkeys;
+    d.r.key_stride = key_stride;
+    d.r.nonces = dnon;
+    d.r.total_bytes_hint = in.arena.size();
+    uint64_t mx = 0;
+    for (size_t i = 0; i < n; ++i) mx = std::max(mx, in.off[i + 1] - in.off[i]);
+    d.r.max_len_hint = (uint32_t)std::min<uint64_t>(mx, 0xffffffffu);
+    return d;
+}
+
+std::vector<std::vector<uint8_t>> download(Staging& st, const DevRecords& d,
+                                           const std::vector<uint64_t>& out_off) {
+    std::vector<uint8_t> all(d.out_total);
+    st.d2h(all.data(), d.out, d.out_total);
+    st.sync();
+    std::vector<std::vector<uint8_t>> res(out_off.size() - 1);
+    for (size_t i = 0; i + 1 < out_off.size(); ++i)
+        res[i].assign(all.begin() + (ptrdiff_t)out_off[i], all.begin() + (ptrdiff_t)out_off[i + 1]);
+    return res;
+}
+
+std::vector<uint8_t> flat_keys(std::span<const ephemeralnet::crypto::Key> keys) {
+    std::vector<uint8_t> v(32 * keys.size());
+    for (size_t i = 0; i < keys.size(); ++i) std::memcpy(v.data() + 32 * i, keys[i].bytes.data(), 32);
+    return v;
+}
+
+std::vector<uint8_t> flat_nonces(std::span<const ephemeralnet::crypto::Nonce> nonces) {
+    std::vector<uint8_t> v(12 * nonces.size());
+    for (size_t i = 0; i < nonces.size(); ++i) std::memcpy(v.data() + 12 * i, nonces[i].bytes.data(), 12);
+    return v;
+}
+
+std::array<uint8_t, 32> one_sha(std::span<const uint8_t> data) {
+    Staging& st = staging();
+    std::span<const uint8_t> items[1] = {data};
+    Packed p = pack(items);
+    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
+    auto* dout = (uint8_t*)st.get(S_OUT, 32);
+    st.h2d(din, p.arena.data(), p.arena.size());
+    st.h2d(doff, p.off.data(), 16);
+    enet_check(enet_sha256_batch(1, din, doff, dout, st.s()), "sha256");
+    std::array<uint8_t, 32> d{};
+    st.d2h(d.data(), dout, 32);
+    st.sync();
+    return d;
+}
+
+}  // namespace
+
+namespace ephemeralnet::crypto {
+
+// ------------------------------------------------------------------------------ ChaCha20
+void ChaCha20::apply(const Key& key, const Nonce& nonce, std::span<const std::uint8_t> input,
+                     std::vector<std::uint8_t>& output, std::uint32_t counter) {
+    if (input.empty()) {  // ChaCha20.cpp:103-108: resize(0), no block generated
+        output.clear();
+        return;
+    }
+    std::span<const uint8_t> items[1] = {input};
+    const std::span<const Key> ks(&key, 1);
+    const std::span<const Nonce> ns(&nonce, 1);
+    const std::uint32_t ctr[1] = {counter};
+    auto res = batch::chacha20_apply(ks, ns, items, ctr);
+    output = std::move(res[0]);
+}
+
+// ------------------------------------------------------------------------------ SHA-256
+Sha256::Sha256() = default;
+
+void Sha256::update(std::span<const std::uint8_t> data) {
+    pending_.insert(pending_.end(), data.begin(), data.end());
+}
+
+std::array<std::uint8_t, 32> Sha256::finalize() {
+    auto d = one_sha(pending_);
+    std::fill(pending_.begin(), pending_.end(), 0);  // finalize resets (Sha256.cpp:122-124)
+    pending_.clear();
+    return d;
+}
+
+std::array<std::uint8_t, 32> Sha256::digest(std::span<const std::uint8_t> data) { return one_sha(data); }
+
+// ------------------------------------------------------------------------------ HMAC
+std::array<std::uint8_t, HmacSha256::kDigestSize> HmacSha256::compute(std::span<const std::uint8_t> key,
+                                                                      std::span<const std::uint8_t> data) {
+    Staging& st = staging();
+    std::span<const uint8_t> items[1] = {data};
+    std::span<const uint8_t> kitems[1] = {key};
+    Packed p = pack(items);
+    Packed k = pack(kitems);
+    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
+    auto* dk = (uint8_t*)st.get(S_KEYS, k.arena.size());
+    auto* dkoff = (uint64_t*)st.get(S_OUTOFF, 16);
+    auto* dout = (uint8_t*)st.get(S_OUT, 32);
+    st.h2d(din, p.arena.data(), p.arena.size());
+    st.h2d(doff, p.off.data(), 16);
+    st.h2d(dk, k.arena.data(), k.arena.size());
+    st.h2d(dkoff, k.off.data(), 16);
+    enet_check(enet_hmac_sha256_batch(1, dk, dkoff, 0, din, doff, dout, st.s()), "hmac");
+    std::array<uint8_t, 32> m{};
+    st.d2h(m.data(), dout, 32);
+    st.sync();
+    return m;
+}
+
+bool HmacSha256::verify(std::span<const std::uint8_t> key, std::span<const std::uint8_t> data,
+                        std::span<const std::uint8_t> mac) {
+    if (mac.size() != kDigestSize) return false;  // HmacSha256.cpp:44
+    Staging& st = staging();
+    std::span<const uint8_t> items[1] = {data};
+    std::span<const uint8_t> kitems[1] = {key};
+    Packed p = pack(items);
+    Packed k = pack(kitems);
+    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
+    auto* dk = (uint8_t*)st.get(S_KEYS, k.arena.size());
+    auto* dkoff = (uint64_t*)st.get(S_OUTOFF, 16);
+    auto* dmac = (uint8_t*)st.get(S_TAGS, 32);
+    auto* dok = (uint8_t*)st.get(S_OK, 4);
+    st.h2d(din, p.arena.data(), p.arena.size());
+    st.h2d(doff, p.off.data(), 16);
+    st.h2d(dk, k.arena.data(), k.arena.size());
+    st.h2d(dkoff, k.off.data(), 16);
+    st.h2d(dmac, mac.data(), 32);
+    enet_check(enet_hmac_sha256_verify_batch(1, dk, dkoff, 0, din, doff, dmac, dok, st.s()), "hmac verify");
+    uint8_t ok = 0;
+    st.d2h(&ok, dok, 1);
+    st.sync();
+    return ok == 1;
+}
+
+// ------------------------------------------------------------------------------ CryptoManager
+namespace {
+std::uint32_t derive_counter(const ChunkId& id) { return enet_chunk_counter(id.data()); }
+
+void fill_random_bytes(std::span<std::uint8_t> buffer) {  // CryptoManager.cpp:17-24
+    std::random_device rd;
+    for (auto& b : buffer) b = static_cast<std::uint8_t>(rd());
+}
+}  // namespace
+
+CryptoManager::CryptoManager() : CryptoManager(Key{}) {}
+
+CryptoManager::CryptoManager(Key key) : key_(key), prng_(std::random_device{}()) {
+    if (std::all_of(key_.bytes.begin(), key_.bytes.end(), [](auto v) { return v == 0U; }))
+        fill_random(key_.bytes);
+}
+
+CipherText CryptoManager::encrypt(const ChunkId& chunk_id, const ChunkData& plaintext) {
+    CipherText out{};
+    fill_random(out.nonce.bytes);
+    ChaCha20::apply(key_, out.nonce, plaintext, out.data, derive_counter(chunk_id));
+    return out;
+}
+
+std::optional<ChunkData> CryptoManager::decrypt(const ChunkId& chunk_id,
+                                                std::span<const std::uint8_t> ciphertext,
+                                                const Nonce& nonce) const {
+    ChunkData pt;
+    ChaCha20::apply(key_, nonce, ciphertext, pt, derive_counter(chunk_id));
+    return pt;
+}
+
+void CryptoManager::fill_random(std::span<std::uint8_t> buffer) const {  // CryptoManager.cpp:60-65
+    std::uniform_int_distribution<std::uint32_t> dist(0, 0xFF);
+    for (auto& b : buffer) b = static_cast<std::uint8_t>(dist(prng_));
+}
+
+Key CryptoManager::generate_key() {
+    Key k{};
+    fill_random_bytes(k.bytes);
+    return k;
+}
+
+void CryptoManager::random_bytes(std::span<std::uint8_t> buffer) { fill_random_bytes(buffer); }
+
+CipherText CryptoManager::encrypt_with_key(const Key& key, const ChunkId& chunk_id, const ChunkData& plaintext) {
+    CryptoManager m{key};
+    return m.encrypt(chunk_id, plaintext);
+}
+
+std::optional<ChunkData> CryptoManager::decrypt_with_key(const Key& key, const ChunkId& chunk_id,
+                                                         std::span<const std::uint8_t> ciphertext,
+                                                         const Nonce& nonce) {
+    CryptoManager m{key};
+    return m.decrypt(chunk_id, ciphertext, nonce);
+}
+
+// ------------------------------------------------------------------------------ batch
+namespace batch {
+
+std::vector<std::vector<std::uint8_t>> chacha20_apply(std::span<const Key> keys, std::span<const Nonce> nonces,
+                                                      std::span<const std::span<const std::uint8_t>> inputs,
+                                                      std::span<const std::uint32_t> counters) {
+    const size_t n = inputs.size();
+    if (keys.size() != n || nonces.size() != n || (!counters.empty() && counters.size() != n))
+        throw std::invalid_argument("enet batch::chacha20_apply: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(inputs);
+    auto kf = flat_keys(keys);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
+    const uint32_t* dctr = nullptr;
+    if (!counters.empty()) {
+        auto* c = (uint32_t*)st.get(S_CTR, 4 * n);
+        st.h2d(c, counters.data(), 4 * n);
+        dctr = c;
+    }
+    enet_check(enet_chacha20_xor_batch(&d.r, dctr, st.s()), "chacha20");
+    return download(st, d, in.off);
+}
+
+std::vector<Sealed> aead_seal(std::span<const Key> keys, std::span<const Nonce> nonces,
+                              std::span<const std::span<const std::uint8_t>> plaintexts) {
+    const size_t n = plaintexts.size();
+    if (keys.size() != n || nonces.size() != n) throw std::invalid_argument("enet batch::aead_seal: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(plaintexts);
+    auto kf = flat_keys(keys);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
+    auto* tags = (uint8_t*)st.get(S_TAGS, 16 * n);
+    enet_check(enet_aead_seal_batch(&d.r, nullptr, nullptr, tags, st.s()), "aead_seal");
+    std::vector<uint8_t> th(16 * n);
+    st.d2h(th.data(), tags, 16 * n);
+    auto data = download(st, d, in.off);
+    std::vector<Sealed> res(n);
+    for (size_t i = 0; i < n; ++i) {
+        res[i].data = std::move(data[i]);
+        std::memcpy(res[i].tag.data(), th.data() + 16 * i, 16);
+    }
+    return res;
+}
+
+std::vector<std::vector<std::uint8_t>> aead_open(std::span<const Key> keys, std::span<const Nonce> nonces,
+                                                 std::span<const std::span<const std::uint8_t>> ciphertexts,
+                                                 std::span<const std::array<std::uint8_t, 16>> tags,
+                                                 std::vector<std::uint8_t>& ok) {
+    const size_t n = ciphertexts.size();
+    if (keys.size() != n || nonces.size() != n || tags.size() != n)
+        throw std::invalid_argument("enet batch::aead_open: size mismatch");
+    ok.assign(n, 0);
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(ciphertexts);
+    auto kf = flat_keys(keys);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
+    auto* dt = (uint8_t*)st.get(S_TAGS, 16 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    st.h2d(dt, tags.data(), 16 * n);
+    enet_check(enet_aead_open_batch(&d.r, nullptr, nullptr, dt, dok, st.s()), "aead_open");
+    st.d2h(ok.data(), dok, n);
+    return download(st, d, in.off);
+}
+
+std::vector<std::array<std::uint8_t, 32>> sha256(std::span<const std::span<const std::uint8_t>> messages) {
+    const size_t n = messages.size();
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(messages);
+    auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
+    auto* dout = (uint8_t*)st.get(S_OUT, 32 * n);
+    st.h2d(din, in.arena.data(), in.arena.size());
+    st.h2d(doff, in.off.data(), 8 * (n + 1));
+    enet_check(enet_sha256_batch((uint32_t)n, din, doff, dout, st.s()), "sha256");
+    std::vector<std::array<std::uint8_t, 32>> res(n);
+    st.d2h(res.data(), dout, 32 * n);
+    st.sync();
+    return res;
+}
+
+std::vector<std::vector<std::uint8_t>> frame_seal(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                                                  std::span<const Nonce> nonces,
+                                                  std::span<const std::span<const std::uint8_t>> messages) {
+    const size_t n = messages.size();
+    if (session_keys.size() != n || nonces.size() != n)
+        throw std::invalid_argument("enet batch::frame_seal: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(messages);
+    auto out_off = offsets_of(messages, 32);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
+    enet_check(enet_frame_seal_batch(&d.r, st.s()), "frame_seal");
+    return download(st, d, out_off);
+}
+
+std::vector<std::vector<std::uint8_t>> frame_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                                                  std::span<const Nonce> nonces,
+                                                  std::span<const std::span<const std::uint8_t>> bodies,
+                                                  std::vector<std::uint8_t>& ok) {
+    const size_t n = bodies.size();
+    if (session_keys.size() != n || nonces.size() != n)
+        throw std::invalid_argument("enet batch::frame_open: size mismatch");
+    ok.assign(n, 0);
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(bodies);
+    auto out_off = offsets_of(bodies, -32);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
+    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    enet_check(enet_frame_open_batch(&d.r, macs, dok, st.s()), "frame_open");
+    st.d2h(ok.data(), dok, n);
+    return download(st, d, out_off);
+}
+
+}  // namespace batch
+}  // namespace ephemeralnet::crypto

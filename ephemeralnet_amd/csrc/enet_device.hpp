@@ -1,0 +1,278 @@
+// enet_device.hpp -- CDNA4 (gfx950) device primitives for the bulk crypto engine.
+//
+// ChaCha20 state words live in VGPRs, one 64-byte block per lane; quarter-rounds are 32-bit
+// ARX (v_add_u32 / v_xor_b32 / v_alignbit_b32).  Poly1305 uses five 26-bit limbs with 64-bit
+// partial products (v_mad_u64_u32).  SHA-256 is one record per lane.  No MFMA anywhere: none of
+// this is a dense contraction.
+//
+// Reference behaviour restated here (file:line into ShardianLabs/EphemeralNet):
+//   ChaCha20 block / quarter round     src/crypto/ChaCha20.cpp:38-94
+//   ChaCha20::apply u32 counter wrap   src/crypto/ChaCha20.cpp:110
+//   SHA-256 compression               src/crypto/Sha256.cpp:134-176
+// Poly1305 has no reference implementation; it follows RFC 8439 2.5.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace enet {
+
+// ----------------------------------------------------------------------------- ChaCha20
+constexpr uint32_t kSigma0 = 0x61707865u, kSigma1 = 0x3320646eu, kSigma2 = 0x79622d32u,
+                   kSigma3 = 0x6b206574u;  // "expand 32-byte k", ChaCha20.cpp:11-16
+
+__device__ __forceinline__ uint32_t rotl(uint32_t v, int s) { return __builtin_rotateleft32(v, s); }
+
+#define ENET_QR(a, b, c, d)                  \
+    do {                                     \
+        a += b; d ^= a; d = rotl(d, 16);     \
+        c += d; b ^= c; b = rotl(b, 12);     \
+        a += b; d ^= a; d = rotl(d, 8);      \
+        c += d; b ^= c; b = rotl(b, 7);      \
+    } while (0)
+
+// Per-record ChaCha20 constants.  The first column round's quarter-rounds on columns 1..3 do
+// not involve the block counter (word 12), so they are computed once per record and reused for
+// every block of that record; only column 0 is recomputed per block.
+struct ChachaRecord {
+    uint32_t k[8];      // key words (feed-forward)
+    uint32_t n[3];      // nonce words (feed-forward)
+    uint32_t pre[12];   // columns 1..3 after the first column round: x1,x5,x9,x13,x2,...,x15
+};
+
+__device__ __forceinline__ void chacha_record_init(ChachaRecord& R, const uint32_t k[8],
+                                                   const uint32_t n[3]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) R.k[i] = k[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) R.n[i] = n[i];
+    uint32_t a1 = kSigma1, b1 = k[1], c1 = k[5], d1 = n[0];
+    uint32_t a2 = kSigma2, b2 = k[2], c2 = k[6], d2 = n[1];
+    uint32_t a3 = kSigma3, b3 = k[3], c3 = k[7], d3 = n[2];
+    ENET_QR(a1, b1, c1, d1);
+    ENET_QR(a2, b2, c2, d2);
+    ENET_QR(a3, b3, c3, d3);
+    R.pre[0] = a1; R.pre[1] = b1; R.pre[2] = c1; R.pre[3] = d1;
+    R.pre[4] = a2; R.pre[5] = b2; R.pre[6] = c2; R.pre[7] = d2;
+    R.pre[8] = a3; R.pre[9] = b3; R.pre[10] = c3; R.pre[11] = d3;
+}
+
+// Keystream block for `counter` (chacha20_block, ChaCha20.cpp:56-94), as 16 LE words.
+__device__ __forceinline__ void chacha_block(const ChachaRecord& R, uint32_t counter,
+                                             uint32_t x[16]) {
+    uint32_t x0 = kSigma0, x4 = R.k[0], x8 = R.k[4], x12 = counter;
+    ENET_QR(x0, x4, x8, x12);
+    uint32_t x1 = R.pre[0], x5 = R.pre[1], x9 = R.pre[2], x13 = R.pre[3];
+    uint32_t x2 = R.pre[4], x6 = R.pre[5], x10 = R.pre[6], x14 = R.pre[7];
+    uint32_t x3 = R.pre[8], x7 = R.pre[9], x11 = R.pre[10], x15 = R.pre[11];
+    // rest of double round 1: diagonal round
+    ENET_QR(x0, x5, x10, x15);
+    ENET_QR(x1, x6, x11, x12);
+    ENET_QR(x2, x7, x8, x13);
+    ENET_QR(x3, x4, x9, x14);
+#pragma unroll
+    for (int i = 1; i < 10; ++i) {
+        ENET_QR(x0, x4, x8, x12);
+        ENET_QR(x1, x5, x9, x13);
+        ENET_QR(x2, x6, x10, x14);
+        ENET_QR(x3, x7, x11, x15);
+        ENET_QR(x0, x5, x10, x15);
+        ENET_QR(x1, x6, x11, x12);
+        ENET_QR(x2, x7, x8, x13);
+        ENET_QR(x3, x4, x9, x14);
+    }
+    x[0] = x0 + kSigma0; x[1] = x1 + kSigma1; x[2] = x2 + kSigma2; x[3] = x3 + kSigma3;
+    x[4] = x4 + R.k[0]; x[5] = x5 + R.k[1]; x[6] = x6 + R.k[2]; x[7] = x7 + R.k[3];
+    x[8] = x8 + R.k[4]; x[9] = x9 + R.k[5]; x[10] = x10 + R.k[6]; x[11] = x11 + R.k[7];
+    x[12] = x12 + counter; x[13] = x13 + R.n[0]; x[14] = x14 + R.n[1]; x[15] = x15 + R.n[2];
+}
+
+// ----------------------------------------------------------------------------- Poly1305
+// Field elements mod 2^130-5 in five 26-bit limbs.  `Pmul` holds a multiplier and its 5x
+// multiples (2^130 == 5), so h*r needs 25 v_mad_u64_u32 and a short carry chain.
+constexpr uint32_t M26 = 0x3ffffffu;
+
+struct Pmul {
+    uint32_t r[5];
+    uint32_t s[5];  // s[i] = 5 * r[i] (s[0] unused)
+};
+
+__device__ __forceinline__ Pmul pmul_make(const uint32_t r[5]) {
+    Pmul m;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) { m.r[i] = r[i]; m.s[i] = r[i] * 5u; }
+    return m;
+}
+
+// h <- h * m (mod 2^130-5), partially reduced: limbs < 2^26 except h1 < 2^26 + 2^6.
+// Inputs: limbs of h < 2^27, limbs of m.r < 2^26 (so the 64-bit sums stay < 2^58).
+__device__ __forceinline__ void pmul(uint32_t h[5], const Pmul& m) {
+    const uint64_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+    uint64_t d0 = h0 * m.r[0] + h1 * m.s[4] + h2 * m.s[3] + h3 * m.s[2] + h4 * m.s[1];
+    uint64_t d1 = h0 * m.r[1] + h1 * m.r[0] + h2 * m.s[4] + h3 * m.s[3] + h4 * m.s[2];
+    uint64_t d2 = h0 * m.r[2] + h1 * m.r[1] + h2 * m.r[0] + h3 * m.s[4] + h4 * m.s[3];
+    uint64_t d3 = h0 * m.r[3] + h1 * m.r[2] + h2 * m.r[1] + h3 * m.r[0] + h4 * m.s[4];
+    uint64_t d4 = h0 * m.r[4] + h1 * m.r[3] + h2 * m.r[2] + h3 * m.r[1] + h4 * m.r[0];
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
+    c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
+    c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
+    c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
+    c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
+    h[0] += c * 5u;
+    c = h[0] >> 26; h[0] &= M26; h[1] += c;
+}
+
+// h += 16-byte block (w0..w3 little-endian words) + hibit * 2^128.
+__device__ __forceinline__ void padd_block(uint32_t h[5], uint32_t w0, uint32_t w1, uint32_t w2,
+                                           uint32_t w3, uint32_t hibit) {
+    h[0] += w0 & M26;
+    h[1] += __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
+    h[2] += __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
+    h[3] += __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
+    h[4] += (w3 >> 8) | (hibit << 24);
+}
+
+// 128-bit value (4 LE words) into limbs, no 2^128 bit.
+__device__ __forceinline__ void plimbs(uint32_t out[5], uint32_t w0, uint32_t w1, uint32_t w2,
+                                       uint32_t w3) {
+    out[0] = w0 & M26;
+    out[1] = __builtin_amdgcn_alignbit(w1, w0, 26) & M26;
+    out[2] = __builtin_amdgcn_alignbit(w2, w1, 20) & M26;
+    out[3] = __builtin_amdgcn_alignbit(w3, w2, 14) & M26;
+    out[4] = w3 >> 8;
+}
+
+// Fully reduce h mod 2^130-5, add the 128-bit pad s, emit the tag as 4 LE words.
+__device__ __forceinline__ void pfinish(const uint32_t hin[5], const uint32_t s[4],
+                                        uint32_t tag[4]) {
+    uint32_t h0 = hin[0], h1 = hin[1], h2 = hin[2], h3 = hin[3], h4 = hin[4], c;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        c = h0 >> 26; h0 &= M26; h1 += c;
+        c = h1 >> 26; h1 &= M26; h2 += c;
+        c = h2 >> 26; h2 &= M26; h3 += c;
+        c = h3 >> 26; h3 &= M26; h4 += c;
+        c = h4 >> 26; h4 &= M26; h0 += c * 5u;
+    }
+    c = h0 >> 26; h0 &= M26; h1 += c;
+    // g = h + 5 - 2^130; use g when it does not borrow (h >= p)
+    uint32_t g0 = h0 + 5u; c = g0 >> 26; g0 &= M26;
+    uint32_t g1 = h1 + c; c = g1 >> 26; g1 &= M26;
+    uint32_t g2 = h2 + c; c = g2 >> 26; g2 &= M26;
+    uint32_t g3 = h3 + c; c = g3 >> 26; g3 &= M26;
+    uint32_t g4 = h4 + c - (1u << 26);
+    const uint32_t use_g = (g4 >> 31) - 1u;  // all ones when no borrow
+    h0 = (h0 & ~use_g) | (g0 & use_g);
+    h1 = (h1 & ~use_g) | (g1 & use_g);
+    h2 = (h2 & ~use_g) | (g2 & use_g);
+    h3 = (h3 & ~use_g) | (g3 & use_g);
+    h4 = (h4 & ~use_g) | (g4 & use_g);
+    // pack to 128 bits and add s mod 2^128
+    uint64_t f;
+    f = (uint64_t)(h0 | (h1 << 26)) + s[0]; tag[0] = (uint32_t)f;
+    f = (uint64_t)((h1 >> 6) | (h2 << 20)) + s[1] + (f >> 32); tag[1] = (uint32_t)f;
+    f = (uint64_t)((h2 >> 12) | (h3 << 14)) + s[2] + (f >> 32); tag[2] = (uint32_t)f;
+    f = (uint64_t)((h3 >> 18) | (h4 << 8)) + s[3] + (f >> 32); tag[3] = (uint32_t)f;
+}
+
+// r clamp (RFC 8439 2.5.1) on the 4 LE words of the one-time key's first half, into limbs.
+__device__ __forceinline__ void pclamp(uint32_t r[5], uint32_t w0, uint32_t w1, uint32_t w2,
+                                       uint32_t w3) {
+    plimbs(r, w0 & 0x0fffffffu, w1 & 0x0ffffffcu, w2 & 0x0ffffffcu, w3 & 0x0ffffffcu);
+}
+
+// ----------------------------------------------------------------------------- SHA-256
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+__device__ __forceinline__ uint32_t rotr(uint32_t v, int s) { return __builtin_rotateright32(v, s); }
+
+__constant__ static const uint32_t kSha256K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+constexpr uint32_t kShaIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+// One compression (Sha256::transform, Sha256.cpp:134-176) on 16 big-endian message words.
+// The 64-entry schedule is kept as a rolling 16-word window in registers.
+__device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+             h = st[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        uint32_t wi;
+        if (i < 16) {
+            wi = w[i];
+        } else {
+            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+            w[i & 15] = wi;
+        }
+        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t t1 = h + S1 + ch + kSha256K[i] + wi;
+        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// ----------------------------------------------------------------------------- byte I/O
+// Load `n` (0..64) bytes at p into 16 LE words, zero beyond n.  Full blocks use four
+// 16-byte loads; the (at most one per record) partial block goes byte by byte.
+__device__ __forceinline__ void load_block(const uint8_t* __restrict__ p, uint32_t n,
+                                           uint32_t w[16]) {
+    if (n >= 64) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 v = q[i];
+            w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+        }
+    } else {
+        // at most one partial block per record: predicated byte loads, compile-time indices
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if ((uint32_t)(4 * i + b) < n) v |= (uint32_t)p[4 * i + b] << (8 * b);
+            w[i] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ void store_block(uint8_t* __restrict__ p, uint32_t n,
+                                            const uint32_t w[16]) {
+    if (n >= 64) {
+        uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if ((uint32_t)(4 * i + b) < n) p[4 * i + b] = (uint8_t)(w[i] >> (8 * b));
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+}  // namespace enet

@@ -1,0 +1,60 @@
+// enet_internal.hpp -- launch-side declarations shared by the kernel TUs and the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace enet {
+
+constexpr int kWG = 256;           // threads per workgroup (4 waves of 64)
+constexpr int kMaxLanesPerRecord = 16;
+
+enum RecMode : int { MODE_XOR = 0, MODE_SEAL = 1, MODE_OPEN = 2 };
+
+// Kernel parameters for the ChaCha20 / AEAD record engine (passed by value).
+struct RecParams {
+    uint32_t n;
+    const uint64_t* in_off;
+    const uint64_t* out_off;
+    const uint8_t* in;
+    uint8_t* out;
+    const uint8_t* keys;
+    uint32_t key_stride;
+    const uint8_t* nonces;
+    const uint32_t* counters;  // MODE_XOR start counters (nullable -> 0)
+    const uint8_t* aad;        // nullable
+    const uint64_t* aad_off;   // nullable
+    const uint8_t* tag_in;     // open: expected tags
+    uint8_t* tag_out;          // seal: produced tags
+    uint8_t* ok;               // open: verdicts
+    const uint32_t* order;     // nullable
+    // frame mode (MODE_XOR over in || mac): when non-null, bytes [len_in, len_in+32) of the
+    // virtual input come from append[32*rec]
+    const uint8_t* append;
+};
+
+// lanes: 1, 2, 4, 8 or 16 lanes per record.
+hipError_t launch_records(int mode, const RecParams& p, uint32_t lanes, hipStream_t s);
+
+struct ShaParams {
+    uint32_t n;
+    const uint8_t* in;
+    const uint64_t* off;
+    uint8_t* digest;           // [n][32], or an arena when dest_off != null
+    const uint64_t* dest_off;  // nullable: digest i goes to digest + dest_off[i] + len_i
+    // HMAC: when keys != null the lane computes HMAC(key_i, msg_i) (HmacSha256.cpp:11-39)
+    const uint8_t* keys;
+    const uint64_t* key_off;   // nullable: fixed 32-byte keys
+    uint32_t key_stride;       // 32 or 0 (shared key) when key_off == null
+    const uint8_t* expect;     // verify: expected MACs [n][32] (nullable -> compute only)
+    uint8_t* ok;               // verify verdicts
+    const uint64_t* guard_off; // verify: records whose guard length is < 32 fail (Message.cpp:315)
+    uint8_t* zero_on_fail;     // verify: arena (indexed like `in`) to zero for failed records
+    const uint32_t* order;     // nullable
+};
+hipError_t launch_sha(const ShaParams& p, hipStream_t s);
+
+
+uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
+
+}  // namespace enet

@@ -1,0 +1,127 @@
+/*
+ * enet_crypto.h -- C ABI of the MI355X bulk crypto engine for EphemeralNet.
+ *
+ * The reference crypto (ShardianLabs/EphemeralNet src/crypto) is a set of static C++20 member
+ * functions taking one record per call.  This ABI is the batched, device-side
+ * form of exactly those operations: every entry point below names the reference interface it
+ * replaces (file:line).  The C++ API in include/ephemeralnet/crypto/ keeps the reference
+ * signatures and is implemented on top of these calls (libenet_crypto.so exports both).
+ *
+ * Conventions
+ *   - All buffer pointers are DEVICE pointers (hipMalloc'd, or any device-accessible memory)
+ *     unless a comment says otherwise.  `stream` is a hipStream_t (NULL = legacy default).
+ *   - Calls are asynchronous on `stream`; nothing is allocated, freed or synchronised inside
+ *     them (safe to capture in a hipGraph).  The caller keeps ownership of every buffer.
+ *   - Records are described SoA: a byte arena plus uint64 offsets[n+1]; record i is
+ *     arena[offsets[i] .. offsets[i+1]).  Input and output arenas have their own offsets so
+ *     length-changing ops (frames: +32-byte MAC) and in-place ops (out == in) both work.
+ *   - keys / nonces / counters / tags / ok arrays must be 4-byte aligned.  Arena offsets may
+ *     be arbitrary; 16-byte-aligned record starts run fastest.
+ *   - Return 0 on success, a negative ENET_E* code otherwise.  Nothing throws across the ABI.
+ *   - Thread-safe: calls on different streams may run concurrently from any host thread.
+ */
+#ifndef ENET_CRYPTO_H
+#define ENET_CRYPTO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifndef ENET_API
+#define ENET_API __attribute__((visibility("default")))
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ENET_OK 0
+#define ENET_EINVAL (-1)   /* bad argument (null pointer, misalignment, n too large) */
+#define ENET_EHIP (-2)     /* a HIP runtime call or kernel launch failed */
+#define ENET_ENODEV (-3)   /* no usable gfx950 device */
+#define ENET_ENOMEM (-4)   /* allocation failed (host-side helpers only) */
+
+/* A batch of independent records (SoA, device pointers). */
+typedef struct enet_records {
+    uint32_t count;             /* n records */
+    const uint64_t* in_offsets; /* [n+1] byte offsets into `in` */
+    const uint64_t* out_offsets;/* [n+1] byte offsets into `out` (may be == in_offsets) */
+    const uint8_t* in;          /* input arena */
+    uint8_t* out;               /* output arena (may be == in for in-place operation) */
+    const uint8_t* keys;        /* [n][32] ChaCha20 keys, or [1][32] when key_stride == 0 */
+    uint32_t key_stride;        /* 32 = per-record key (per-peer sessions), 0 = one shared key */
+    const uint8_t* nonces;      /* [n][12] 96-bit nonces */
+    const uint32_t* order;      /* optional [n] processing order (e.g. records sorted by length,
+                                   longest first); NULL = 0..n-1.  Results are position-indexed
+                                   either way. */
+    uint64_t total_bytes_hint;  /* host-known sum of input lengths, 0 = unknown (scheduling) */
+    uint32_t max_len_hint;      /* host-known max record length, 0 = unknown (scheduling) */
+} enet_records;
+
+/* ---- ChaCha20 (reference: ChaCha20::apply, src/crypto/ChaCha20.cpp:98-121,
+ *      include/ephemeralnet/crypto/ChaCha20.hpp:20-24)
+ * out_i = in_i XOR keystream(key_i, nonce_i, counters[i], counters[i]+1, ...) with the
+ * reference's uint32 counter wrap (ChaCha20.cpp:110).  counters == NULL means all zero
+ * (SessionManager.cpp:374/822 frames); CryptoManager passes LE32(chunk_id)
+ * (CryptoManager.cpp:8-13, see enet_chunk_counter). */
+ENET_API int enet_chacha20_xor_batch(const enet_records* r, const uint32_t* counters, void* stream);
+
+/* ---- RFC 8439 AEAD_CHACHA20_POLY1305 (promised by the reference README.md:49, not
+ *      implemented there -- SURVEY.md 0.1).  Keystream = ChaCha20::apply(counter = 1), one-time
+ *      Poly1305 key = block(counter = 0).  aad/aad_offsets may be NULL (no AAD).
+ * seal: out_i = ciphertext, tags[i] = 16-byte tag.
+ * open: out_i = plaintext, ok[i] = 1 if the tag verified, else 0 and out_i is zeroed. */
+ENET_API int enet_aead_seal_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
+                         uint8_t* tags, void* stream);
+ENET_API int enet_aead_open_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
+                         const uint8_t* tags, uint8_t* ok, void* stream);
+
+/* ---- SHA-256 (reference: Sha256::digest, src/crypto/Sha256.cpp:128-132)
+ * digests[i] = SHA-256(in[offsets[i]..offsets[i+1])).  Used for chunk ids / manifest hashes
+ * (StoreProof.cpp:75-78, Node.cpp:1414, Node.cpp:1652). */
+ENET_API int enet_sha256_batch(uint32_t n, const uint8_t* in, const uint64_t* offsets, uint8_t* digests,
+                      void* stream);
+
+/* ---- HMAC-SHA256 (reference: HmacSha256::compute / verify, src/crypto/HmacSha256.cpp:11-54)
+ * Key of record i = keys[key_offsets[i] .. key_offsets[i+1]) (keys over 64 B are hashed first,
+ * HmacSha256.cpp:15-17); key_offsets == NULL means fixed 32-byte keys at keys + 32*i, or one
+ * shared 32-byte key when key_stride == 0.
+ * compute: macs[i] = HMAC(key_i, msg_i).
+ * verify : ok[i] = (HMAC(key_i, msg_i) == macs[i]) (constant-time OR-accumulate, :47-53). */
+ENET_API int enet_hmac_sha256_batch(uint32_t n, const uint8_t* keys, const uint64_t* key_offsets,
+                           uint32_t key_stride, const uint8_t* in, const uint64_t* offsets,
+                           uint8_t* macs, void* stream);
+ENET_API int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, const uint64_t* key_offsets,
+                                  uint32_t key_stride, const uint8_t* in,
+                                  const uint64_t* offsets, const uint8_t* macs, uint8_t* ok,
+                                  void* stream);
+
+/* ---- Session frame body (reference: protocol::encode_signed, src/protocol/Message.cpp:305-311
+ *      followed by SessionManager::send, src/network/SessionManager.cpp:362-374; CLI twin
+ *      send_protocol_message, src/main.cpp:1141-1147).
+ * seal: out_i = ChaCha20_{key_i, nonce_i, ctr 0}(in_i || HMAC-SHA256_{key_i}(in_i)),
+ *       |out_i| = |in_i| + 32 (out_offsets must say so).  Keys are the 32-byte session keys.
+ * open (SessionManager.cpp:815-822 then Message.cpp:313-328): out_i = first |in_i|-32 bytes of
+ *       the decryption (out_offsets must say |in_i|-32, or 0 when |in_i| < 32), macs[i] = the
+ *       decrypted 32-byte MAC ([n][32] device buffer), ok[i] = MAC verified (records shorter
+ *       than 32 bytes fail, Message.cpp:315); on failure out_i is zeroed.  The 16-byte wire
+ *       header nonce || BE32(len) (SessionManager.cpp:376-387) is host framing. */
+ENET_API int enet_frame_seal_batch(const enet_records* r, void* stream);
+ENET_API int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
+
+/* ---- helpers (host) */
+/* LE32(chunk_id[0..3]) -- CryptoManager.cpp:8-13 derive_counter. */
+ENET_API uint32_t enet_chunk_counter(const uint8_t chunk_id[32]);
+/* Lanes the scheduler gives each record for a batch of this shape (for tests / tuning). */
+ENET_API uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t max_len);
+/* Force lanes per record (1, 2, 4, 8 or 16) for all later calls in this process; 0 restores the
+ * scheduler.  Returns ENET_EINVAL for other values.  Tuning / test knob. */
+ENET_API int enet_set_lanes_per_record(uint32_t lanes);
+/* Human-readable text of the last error on this host thread ("" if none). */
+ENET_API const char* enet_last_error(void);
+/* ABI version: (major << 16) | minor. */
+ENET_API uint32_t enet_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENET_CRYPTO_H */

@@ -1,0 +1,342 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the golden vectors (compiled reference
+src/crypto; OpenSSL + RFC 8439 for the AEAD) and the CPU oracle on seeded random batches.
+Integer/byte work: every comparison is bit-exact."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle
+from util import splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+
+LANES = [1, 2, 4, 8, 16]
+
+
+@pytest.fixture(scope="module")
+def enet():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import ephemeralnet_amd as E
+    E.lib()
+    yield E
+    E.set_lanes_per_record(0)
+
+
+def dev(b: bytes):
+    import torch
+    return torch.frombuffer(bytearray(b if b else b"\0"), dtype=torch.uint8)[: len(b)].cuda()
+
+
+def host(t) -> bytes:
+    return t.cpu().numpy().tobytes()
+
+
+def expect(rep, got: bytes):
+    if "hex" in rep:
+        assert got.hex() == rep["hex"]
+    else:
+        assert hashlib.sha256(got).hexdigest() == rep["sha256"]
+
+
+def records_of(arena_bytes: bytes, offs):
+    return [arena_bytes[offs[i]:offs[i + 1]] for i in range(len(offs) - 1)]
+
+
+def out_like(b):
+    import torch
+    return torch.zeros_like(b.arena)
+
+
+def rand_lengths(seed, n, hi):
+    raw = np.frombuffer(splitmix_bytes(seed, 4 * n), dtype="<u4")
+    return [int(x % (hi + 1)) for x in raw]
+
+
+# ------------------------------------------------------------------------------ ChaCha20
+@pytest.mark.parametrize("lanes", LANES)
+def test_chacha20_golden(enet, golden, lanes):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    cs = golden["chacha20"]
+    items = [splitmix_bytes(c["pt_seed"], c["len"]) for c in cs]
+    b = enet.make_batch(items, [bytes.fromhex(c["key"]) for c in cs],
+                        [bytes.fromhex(c["nonce"]) for c in cs])
+    ctr = torch.tensor(np.array([c["counter"] for c in cs], dtype=np.uint32).view(np.int32)).cuda()
+    out = out_like(b)
+    enet.chacha20_xor(b, out, counters=ctr)
+    torch.cuda.synchronize()
+    offs = b.offsets.cpu().tolist()
+    got = records_of(host(out), offs)
+    for c, g in zip(cs, got):
+        expect(c["ct"], g)
+
+
+def test_chacha20_rfc8439(enet, golden):
+    import torch
+    v = golden["rfc8439_2_4_2"]
+    b = enet.make_batch([bytes.fromhex(v["pt"])], [bytes.fromhex(v["key"])], [bytes.fromhex(v["nonce"])])
+    out = out_like(b)
+    ctr = torch.tensor([1], dtype=torch.int32).cuda()
+    enet.chacha20_xor(b, out, counters=ctr)
+    assert host(out).hex() == v["ct"]
+
+
+@pytest.mark.parametrize("lanes", LANES)
+@pytest.mark.parametrize("base", [0, 3])
+def test_chacha20_random_vs_oracle(enet, lanes, base):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 300
+    lens = rand_lengths(11 + lanes, n, 5000)
+    lens[:6] = [0, 1, 63, 64, 65, 4096]
+    items = [splitmix_bytes(100 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(10000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(20000 + i, 12) for i in range(n)]
+    ctrs = np.frombuffer(splitmix_bytes(7, 4 * n), dtype="<u4").copy()
+    ctrs[:4] = [0xFFFFFFFF, 0xFFFFFFFE, 0xFFFFFFC0, 0]
+    b = enet.make_batch(items, keys, nonces, base_offset=base)
+    out = out_like(b)
+    enet.chacha20_xor(b, out, counters=torch.tensor(ctrs.view(np.int32)).cuda())
+    got = records_of(host(out), b.offsets.cpu().tolist())
+    for i in range(n):
+        assert got[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctrs[i])), i
+
+
+def test_chacha20_in_place_shared_key(enet):
+    import torch
+    enet.set_lanes_per_record(0)
+    n = 64
+    items = [splitmix_bytes(300 + i, 4096) for i in range(n)]
+    key = splitmix_bytes(1, 32)
+    nonces = [splitmix_bytes(400 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, [key], nonces, key_stride=0)
+    enet.chacha20_xor(b, b.arena)  # in place, counter 0 (SessionManager.cpp:374)
+    got = records_of(host(b.arena), b.offsets.cpu().tolist())
+    for i in range(n):
+        assert got[i] == oracle.chacha20_xor(key, nonces[i], items[i], 0)
+
+
+def test_cryptomanager_golden(enet, golden):
+    import torch
+    cs = golden["cryptomanager"]
+    items = [splitmix_bytes(c["pt_seed"], c["len"]) for c in cs]
+    b = enet.make_batch(items, [bytes.fromhex(c["key"]) for c in cs], [bytes.fromhex(c["nonce"]) for c in cs])
+    ctr = np.array([enet.chunk_counter(bytes.fromhex(c["chunk_id"])) for c in cs], dtype=np.uint32)
+    out = out_like(b)
+    enet.chacha20_xor(b, out, counters=torch.tensor(ctr.view(np.int32)).cuda())
+    for c, g in zip(cs, records_of(host(out), b.offsets.cpu().tolist())):
+        expect(c["ct"], g)
+
+
+# ------------------------------------------------------------------------------ AEAD
+def aead_batch(enet, cases, base=0):
+    import torch
+    items = [splitmix_bytes(c["pt_seed"], c["len"]) for c in cases]
+    aads = [splitmix_bytes(c["aad_seed"], c["aad_len"]) for c in cases]
+    b = enet.make_batch(items, [bytes.fromhex(c["key"]) for c in cases],
+                        [bytes.fromhex(c["nonce"]) for c in cases], base_offset=base)
+    aoff = np.concatenate([[0], np.cumsum([len(a) for a in aads])]).astype(np.int64)
+    aad = dev(b"".join(aads) or b"\0")
+    return items, aads, b, aad, torch.tensor(aoff).cuda()
+
+
+@pytest.mark.parametrize("lanes", LANES)
+def test_aead_golden(enet, golden, lanes):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    cs = golden["aead"]
+    items, aads, b, aad, aoff = aead_batch(enet, cs)
+    out = out_like(b)
+    tags = torch.zeros(16 * len(cs), dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags, aad, aoff)
+    offs = b.offsets.cpu().tolist()
+    got = records_of(host(out), offs)
+    th = host(tags)
+    for i, c in enumerate(cs):
+        expect(c["ct"], got[i])
+        assert th[16 * i:16 * i + 16].hex() == c["tag"], (i, c["len"], c["aad_len"])
+    # open the ciphertext back, one tampered record and one tampered tag
+    ct = out.clone()
+    tags2 = tags.clone()
+    tamper_rec = next(i for i, c in enumerate(cs) if c["len"] >= 64)
+    ct[offs[tamper_rec] + 5] ^= 1
+    tags2[16 * 2] ^= 0x40
+    b2 = enet.Batch(ct, b.offsets, b.keys, b.nonces, total_bytes_hint=b.total_bytes_hint,
+                    max_len_hint=b.max_len_hint)
+    pt = torch.full_like(ct, 0xAA)
+    ok = torch.zeros(len(cs), dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, pt, tags2, ok, aad, aoff)
+    okh = ok.cpu().tolist()
+    back = records_of(host(pt), offs)
+    for i in range(len(cs)):
+        if i in (tamper_rec, 2):
+            assert okh[i] == 0
+            assert back[i] == bytes(len(back[i]))  # plaintext not released
+        else:
+            assert okh[i] == 1, i
+            assert back[i] == items[i]
+
+
+def test_aead_rfc8439(enet, golden):
+    import torch
+    v = golden["rfc8439_2_8_2"]
+    b = enet.make_batch([bytes.fromhex(v["pt"])], [bytes.fromhex(v["key"])], [bytes.fromhex(v["nonce"])])
+    aad = dev(bytes.fromhex(v["aad"]))
+    aoff = torch.tensor([0, 12], dtype=torch.int64).cuda()
+    out = out_like(b)
+    tags = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags, aad, aoff)
+    assert host(out).hex() == v["ct"]
+    assert host(tags).hex() == v["tag"] == "1ae10b594f09e26a7e902ecbd0600691"
+
+
+@pytest.mark.parametrize("lanes", LANES)
+@pytest.mark.parametrize("base", [0, 5])
+def test_aead_random_vs_oracle(enet, lanes, base):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 257
+    lens = rand_lengths(50 + lanes, n, 3000)
+    lens[:8] = [0, 1, 15, 16, 17, 64, 1500, 4096]
+    items = [splitmix_bytes(600 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(30000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(40000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces, base_offset=base)
+    out = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    got = records_of(host(out), b.offsets.cpu().tolist())
+    th = host(tags)
+    for i in range(n):
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct, i
+        assert th[16 * i:16 * i + 16] == tag, (i, lens[i])
+
+
+def test_aead_roundtrip_headline_size(enet):
+    """C2 shape at full size (65 536 x 4 KiB, per-record keys): size-independent properties --
+    open(seal(x)) == x with every tag verified, one flipped bit rejected, and a 512-record
+    sample checked bit-exact against the oracle."""
+    import torch
+    enet.set_lanes_per_record(0)
+    n, L = 65536, 4096
+    g = torch.Generator(device="cuda").manual_seed(2)
+    pt = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device="cuda", generator=g)
+    nonces = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, device="cuda", generator=g)
+    offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device="cuda")
+    b = enet.Batch(pt, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+    ct = torch.empty_like(pt)
+    tags = torch.empty(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, ct, tags)
+    back = torch.empty_like(pt)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    b2 = enet.Batch(ct, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+    ct[12345 * L + 77] ^= 4
+    enet.aead_open(b2, back, tags, ok)
+    okh = ok.cpu()
+    assert int(okh.sum()) == n - 1 and int(okh[12345]) == 0
+    assert torch.equal(back.view(n, L)[:12345], pt.view(n, L)[:12345])
+    assert torch.equal(back.view(n, L)[12346:], pt.view(n, L)[12346:])
+    ct[12345 * L + 77] ^= 4
+    idx = np.linspace(0, n - 1, 512).astype(int)
+    pth, cth, kh, nh, th = (t.cpu().numpy() for t in (pt, ct, keys, nonces, tags))
+    for i in idx:
+        c, t = oracle.aead_seal(kh[32 * i:32 * i + 32].tobytes(), nh[12 * i:12 * i + 12].tobytes(),
+                                pth[i * L:(i + 1) * L].tobytes())
+        assert cth[i * L:(i + 1) * L].tobytes() == c
+        assert th[16 * i:16 * i + 16].tobytes() == t
+
+
+# ------------------------------------------------------------------------------ SHA / HMAC
+def test_sha256_golden(enet, golden):
+    import torch
+    cs = golden["sha256"]
+    items = [b"abc" if c["abc"] else splitmix_bytes(c["seed"], c["len"]) for c in cs]
+    offs = np.concatenate([[0], np.cumsum([len(x) for x in items])]).astype(np.int64)
+    arena = dev(b"".join(items))
+    dig = torch.zeros(32 * len(cs), dtype=torch.uint8, device="cuda")
+    enet.sha256(arena, torch.tensor(offs).cuda(), dig)
+    dh = host(dig)
+    for i, c in enumerate(cs):
+        assert dh[32 * i:32 * i + 32].hex() == c["digest"], c["len"]
+
+
+def test_hmac_golden(enet, golden):
+    import torch
+    cs = golden["hmac"]
+    items = [splitmix_bytes(c["seed"], c["len"]) for c in cs]
+    keys = [bytes.fromhex(c["key"]) for c in cs]
+    offs = np.concatenate([[0], np.cumsum([len(x) for x in items])]).astype(np.int64)
+    koffs = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.int64)
+    arena, karena = dev(b"".join(items)), dev(b"".join(keys) or b"\0")
+    macs = torch.zeros(32 * len(cs), dtype=torch.uint8, device="cuda")
+    to, tk = torch.tensor(offs).cuda(), torch.tensor(koffs).cuda()
+    enet.hmac_sha256(karena, arena, to, macs, key_offsets=tk)
+    mh = host(macs)
+    for i, c in enumerate(cs):
+        assert mh[32 * i:32 * i + 32].hex() == c["mac"], (len(keys[i]), c["len"])
+    # verify: all good, then one corrupted
+    ok = torch.zeros(len(cs), dtype=torch.uint8, device="cuda")
+    macs[32 * 3] ^= 1
+    enet.hmac_sha256_verify(karena, arena, to, macs, ok, key_offsets=tk)
+    okh = ok.cpu().tolist()
+    assert okh[3] == 0 and sum(okh) == len(cs) - 1
+
+
+# ------------------------------------------------------------------------------ frames
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_frames_golden(enet, golden, lanes):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    fs = golden["frames"]
+    msgs = [bytes.fromhex(f["signed"])[:-32] for f in fs]
+    keys = [bytes.fromhex(f["key"]) for f in fs]
+    nonces = [bytes.fromhex(f["nonce"]) for f in fs]
+    b = enet.make_batch(msgs, keys, nonces)
+    ooffs = np.concatenate([[0], np.cumsum([len(m) + 32 for m in msgs])]).astype(np.int64)
+    out = torch.zeros(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
+    to = torch.tensor(ooffs).cuda()
+    enet.frame_seal(b, out, to)
+    bodies = records_of(host(out), ooffs.tolist())
+    for f, body in zip(fs, bodies):
+        assert body.hex() == f["body"]
+    # open: good frames, one tampered, one too short
+    bodies[1] = bytes([bodies[1][0] ^ 1]) + bodies[1][1:]
+    bodies.append(b"\x01" * 20)
+    keys.append(keys[0])
+    nonces.append(nonces[0])
+    bo = enet.make_batch(bodies, keys, nonces)
+    poffs = np.concatenate([[0], np.cumsum([max(len(x) - 32, 0) for x in bodies])]).astype(np.int64)
+    pt = torch.full((max(int(poffs[-1]), 1),), 0xAA, dtype=torch.uint8, device="cuda")
+    macs = torch.zeros(32 * len(bodies), dtype=torch.uint8, device="cuda")
+    ok = torch.zeros(len(bodies), dtype=torch.uint8, device="cuda")
+    enet.frame_open(bo, pt, torch.tensor(poffs).cuda(), macs, ok)
+    okh = ok.cpu().tolist()
+    got = records_of(host(pt), poffs.tolist())
+    for i in range(len(bodies)):
+        if i in (1, len(bodies) - 1):
+            assert okh[i] == 0
+            assert got[i] == bytes(len(got[i]))
+        else:
+            assert okh[i] == 1 and got[i] == msgs[i]
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 16])
+def test_frames_random_vs_oracle(enet, lanes):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 200
+    lens = rand_lengths(77, n, 2100)
+    msgs = [splitmix_bytes(900 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(50000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(60000 + i, 12) for i in range(n)]
+    b = enet.make_batch(msgs, keys, nonces, base_offset=1)
+    ooffs = np.concatenate([[0], np.cumsum([L + 32 for L in lens])]).astype(np.int64)
+    out = torch.zeros(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
+    enet.frame_seal(b, out, torch.tensor(ooffs).cuda())
+    bodies = records_of(host(out), ooffs.tolist())
+    for i in range(n):
+        assert bodies[i] == oracle.frame_seal(keys[i], nonces[i], msgs[i]), i
