@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate wall budget of the CPU baseline sample")
-    ap.add_argument("--verify", action="store_true", help="check ok flags after the timed region")
+    ap.add_argument("--mode", default="aead", choices=["aead", "xor"],
+                    help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline probe)")
     return ap.parse_args()
 
 
@@ -130,10 +131,16 @@ def main():
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        E.aead_seal(seal_b, ct, tags, stream=stream)
+        if args.mode == "aead":
+            E.aead_seal(seal_b, ct, tags, stream=stream)
+        else:
+            E.chacha20_xor(seal_b, ct, stream=stream)
         if ev:
             ev[1].record(stream)
-        E.aead_open(open_b, back, tags, ok, stream=stream)
+        if args.mode == "aead":
+            E.aead_open(open_b, back, tags, ok, stream=stream)
+        else:
+            E.chacha20_xor(open_b, back, stream=stream)
         if ev:
             ev[2].record(stream)
 
@@ -159,7 +166,7 @@ def main():
 
     seal_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     open_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    okh = int(ok.sum().item())
+    okh = int(ok.sum().item()) if args.mode == "aead" else n
     if okh != n:
         raise SystemExit(f"rank {rank}: {n - okh} records failed to open")
 

@@ -59,6 +59,15 @@ enet::RecParams rec_params(const enet_records* r) {
     p.key_stride = r->key_stride;
     p.nonces = r->nonces;
     p.order = r->order;
+    // hints say every record has the same length: total == n * max (record i then starts at
+    // offsets[0] + i * max, since records are contiguous by construction)
+    if (r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint)
+        p.uniform_len = r->max_len_hint;
+    static const int coop_env = [] {
+        const char* s = std::getenv("ENET_COOP");
+        return s ? std::atoi(s) : 1;
+    }();
+    p.coop = coop_env;
     return p;
 }
 

@@ -182,6 +182,83 @@ __device__ __forceinline__ void pclamp(uint32_t r[5], uint32_t w0, uint32_t w1, 
     plimbs(r, w0 & 0x0fffffffu, w1 & 0x0ffffffcu, w2 & 0x0ffffffcu, w3 & 0x0ffffffcu);
 }
 
+// Radix-2^32 Horner step with the CLAMPED r (RFC 8439 clamp clears the top 4 bits of every r
+// word and the low 2 bits of r1..r3).  That makes s_j = r_j + (r_j >> 2) = 5*r_j/4 exact and
+// keeps every column sum below 2^63, so h*r needs 16+4 v_mad_u64_u32 and the column carries
+// ride inside the multiply-add chains (the same construction as OpenSSL's 32-bit Poly1305).
+// h = (h + m + hibit*2^128) * r, partially reduced (h4 <= 4).
+struct PolyR32 {
+    uint32_t r0, r1, r2, r3, s1, s2, s3;
+};
+
+__device__ __forceinline__ PolyR32 polyr32_make(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    PolyR32 R;
+    R.r0 = w0 & 0x0fffffffu;
+    R.r1 = w1 & 0x0ffffffcu;
+    R.r2 = w2 & 0x0ffffffcu;
+    R.r3 = w3 & 0x0ffffffcu;
+    R.s1 = R.r1 + (R.r1 >> 2);
+    R.s2 = R.r2 + (R.r2 >> 2);
+    R.s3 = R.r3 + (R.r3 >> 2);
+    return R;
+}
+
+__device__ __forceinline__ void poly32_block(uint32_t h[5], const PolyR32& R, uint32_t m0,
+                                             uint32_t m1, uint32_t m2, uint32_t m3,
+                                             uint32_t hibit) {
+    // carries ride on 32-bit add-with-carry (v_add_co / v_addc_co); 64-bit adds of zero-extended
+    // words would cost a v_mov per operand
+    unsigned cy;
+    const uint32_t a0 = __builtin_addc(h[0], m0, 0u, &cy);
+    const uint32_t a1 = __builtin_addc(h[1], m1, cy, &cy);
+    const uint32_t a2 = __builtin_addc(h[2], m2, cy, &cy);
+    const uint32_t a3 = __builtin_addc(h[3], m3, cy, &cy);
+    const uint32_t a4 = h[4] + hibit + cy;
+    const uint64_t d0 = (uint64_t)a0 * R.r0 + (uint64_t)a1 * R.s3 + (uint64_t)a2 * R.s2 +
+                        (uint64_t)a3 * R.s1;
+    const uint64_t e1 = (uint64_t)a0 * R.r1 + (uint64_t)a1 * R.r0 + (uint64_t)a2 * R.s3 +
+                        (uint64_t)a3 * R.s2 + (uint64_t)a4 * R.s1;
+    const uint64_t e2 = (uint64_t)a0 * R.r2 + (uint64_t)a1 * R.r1 + (uint64_t)a2 * R.r0 +
+                        (uint64_t)a3 * R.s3 + (uint64_t)a4 * R.s2;
+    const uint64_t e3 = (uint64_t)a0 * R.r3 + (uint64_t)a1 * R.r2 + (uint64_t)a2 * R.r1 +
+                        (uint64_t)a3 * R.r0 + (uint64_t)a4 * R.s3;
+    const uint32_t x0 = (uint32_t)d0;
+    const uint32_t x1 = __builtin_addc((uint32_t)e1, (uint32_t)(d0 >> 32), 0u, &cy);
+    const uint32_t c1 = (uint32_t)(e1 >> 32) + cy;
+    const uint32_t x2 = __builtin_addc((uint32_t)e2, c1, 0u, &cy);
+    const uint32_t c2 = (uint32_t)(e2 >> 32) + cy;
+    const uint32_t x3 = __builtin_addc((uint32_t)e3, c2, 0u, &cy);
+    const uint32_t c3 = (uint32_t)(e3 >> 32) + cy;
+    const uint32_t t4 = a4 * R.r0 + c3;  // < 2^31.6
+    const uint32_t f = (t4 >> 2) * 5u;   // fold 2^130 == 5; < 2^31.9
+    h[0] = __builtin_addc(x0, f, 0u, &cy);
+    h[1] = __builtin_addc(x1, 0u, cy, &cy);
+    h[2] = __builtin_addc(x2, 0u, cy, &cy);
+    h[3] = __builtin_addc(x3, 0u, cy, &cy);
+    h[4] = (t4 & 3u) + cy;
+}
+
+// Radix-2^32 accumulator (h4 small) -> five 26-bit limbs (limb 4 < 2^27).
+__device__ __forceinline__ void h32_to_limbs(const uint32_t h[5], uint32_t l[5]) {
+    l[0] = h[0] & M26;
+    l[1] = __builtin_amdgcn_alignbit(h[1], h[0], 26) & M26;
+    l[2] = __builtin_amdgcn_alignbit(h[2], h[1], 20) & M26;
+    l[3] = __builtin_amdgcn_alignbit(h[3], h[2], 14) & M26;
+    l[4] = (h[3] >> 8) | (h[4] << 24);
+}
+
+// x = r^e (e >= 1), general radix-2^26 square-and-multiply, left to right.
+__device__ __forceinline__ void ppow(const uint32_t r[5], uint32_t e, uint32_t x[5]) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) x[i] = r[i];
+    const Pmul mr = pmul_make(r);
+    const int top = 31 - __builtin_clz(e);
+    for (int b = top - 1; b >= 0; --b) {
+        pmul(x, pmul_make(x));
+        if ((e >> b) & 1u) pmul(x, mr);
+    }
+}
+
 // ----------------------------------------------------------------------------- SHA-256
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 __device__ __forceinline__ uint32_t rotr(uint32_t v, int s) { return __builtin_rotateright32(v, s); }

@@ -31,6 +31,9 @@ struct RecParams {
     // frame mode (MODE_XOR over in || mac): when non-null, bytes [len_in, len_in+32) of the
     // virtual input come from append[32*rec]
     const uint8_t* append;
+    // uniform batch: every record is exactly uniform_len bytes in and out (0 = not uniform)
+    uint64_t uniform_len;
+    int coop;  // allow the cooperative-staging path for uniform batches
 };
 
 // lanes: 1, 2, 4, 8 or 16 lanes per record.

@@ -1,14 +1,13 @@
 // records.hip -- the ChaCha20 / ChaCha20-Poly1305 record engine (gfx950).
 //
 // One wave = 64 lanes; each record gets P lanes (P = 1..16, a power of two chosen by the host
-// scheduler so the chip holds >= 2 waves per SIMD).  Lane j of a record processes ChaCha20
-// blocks j, j+P, j+2P, ... -- one 64-byte block per lane per round, the 4x4 state in VGPRs.
+// scheduler from the batch shape).  Lane j of a record processes a contiguous run of ChaCha20
+// blocks -- one 64-byte block per lane per step, the 4x4 state in VGPRs, the next block's
+// 64 bytes prefetched into registers while the current keystream is computed.
 //
-// Poly1305 (seal / open) runs in the same lanes, interleaved by 16-byte block: lane j owns the
-// Poly1305 stream blocks s == j (mod P) and keeps a Horner accumulator in the multiplier r^P;
-// at the end each lane multiplies by r^(e_j) (e_j in [1, P]) and the P lanes add up their
-// contributions with cross-lane shuffles.  For P > 1 each round's ciphertext is exchanged
-// through a wave-private LDS slab (80-byte lane slots: conflict-free b128 writes and reads).
+// Poly1305 (seal / open) runs in the same lanes over the same bytes: Horner in the clamped r
+// with radix-2^32 limbs (20 v_mad_u64_u32 per 16-byte block), then one r^e scale per lane and
+// a cross-lane sum of the P partial accumulators.  No LDS: every lane MACs its own bytes.
 //
 // Reference behaviour (ShardianLabs/EphemeralNet):
 //   ChaCha20::apply           src/crypto/ChaCha20.cpp:98-121 (u32 counter wrap :110)
@@ -21,43 +20,8 @@
 
 namespace enet {
 
-constexpr int kSlot = 80;  // LDS bytes per lane (64 data + 16 pad)
-
 // Frame sub-modes of MODE_XOR
 enum FrameKind : int { FR_NONE = 0, FR_SEAL = 1, FR_OPEN = 2 };
-
-// r^(2^b) table and the small power r^e, e in [1, 2^LOGP]
-template <int LOGP>
-__device__ __forceinline__ void poly_powers(const uint32_t r[5], Pmul& RP, Pmul& E, uint32_t e) {
-    uint32_t pw[LOGP + 1][5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i) pw[0][i] = r[i];
-#pragma unroll
-    for (int b = 1; b <= LOGP; ++b) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) pw[b][i] = pw[b - 1][i];
-        pmul(pw[b], pmul_make(pw[b - 1]));
-    }
-    RP = pmul_make(pw[LOGP]);
-    if (LOGP == 0) {
-        E = RP;
-        return;
-    }
-    // x = r^e by binary powering over the table (e == 2^LOGP handled by the top bit)
-    uint32_t x[5] = {1, 0, 0, 0, 0};
-#pragma unroll
-    for (int b = 0; b <= LOGP; ++b) {
-        if ((e >> b) & 1u) {
-            uint32_t y[5];
-#pragma unroll
-            for (int i = 0; i < 5; ++i) y[i] = x[i];
-            pmul(y, pmul_make(pw[b]));
-#pragma unroll
-            for (int i = 0; i < 5; ++i) x[i] = y[i];
-        }
-    }
-    E = pmul_make(x);
-}
 
 __device__ __forceinline__ void mask_tail(uint32_t w[16], uint32_t n) {
     // zero bytes >= n of a 64-byte block (n < 64)
@@ -72,12 +36,57 @@ __device__ __forceinline__ void mask_tail(uint32_t w[16], uint32_t n) {
     }
 }
 
-template <int LOGP, int MODE, int FRAME>
+__device__ __forceinline__ void load_full(const uint8_t* __restrict__ p, uint32_t w[16]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = q[i];
+        w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void store_full(uint8_t* __restrict__ p, const uint32_t w[16]) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+// Four Poly1305 blocks (one 64-byte ciphertext block), all full.
+__device__ __forceinline__ void poly_block64(uint32_t h[5], const PolyR32& R, const uint32_t ct[16]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        poly32_block(h, R, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
+}
+
+// Lane layout: record = P consecutive lanes; lane j owns the contiguous ChaCha20 blocks
+// [j*B, min((j+1)*B, nb)), B = ceil(nb / P), and with them the contiguous Poly1305 stream
+// blocks they cover (lane 0 also the AAD prefix, the lane with the last block also the length
+// block).  Each lane runs Horner in the clamped r (radix 2^32); at the end lane j scales its
+// accumulator by r^(N-1-s_last_j) and the P lanes add up with cross-lane shuffles.
+// COOP (uniform batches only: every record has the same length, so record g starts at
+// in_off[0] + g*L): whole-block stages of kStage blocks per lane are moved wave-cooperatively.
+// Load instruction i of a stage serves owners 8i..8i+7 of the wave (64 lanes x 16 B = 8 owners x
+// 128 contiguous bytes = whole 128-byte lines), lands in a wave-private LDS slab
+// [owner][128 B] whose 16-byte chunks are XOR-swizzled by (owner >> 1) & 7 (conflict-free
+// ds_read_b128), and each lane then reads its own two blocks.  Outputs take the reverse trip.
+// Within one wave, DS instructions execute in issue order, so handing LDS data between lanes
+// of the same wave needs only a compiler barrier -- a wavefront-scope fence would also drain the
+// in-flight global loads/stores (s_waitcnt vmcnt(0)) and serialise every stage.
+#define ENET_WAVE_LDS_SYNC()                  \
+    do {                                      \
+        asm volatile("" ::: "memory");        \
+        __builtin_amdgcn_wave_barrier();      \
+        asm volatile("" ::: "memory");        \
+    } while (0)
+
+constexpr uint32_t kStage = 2;                 // blocks per lane per cooperative stage
+constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
+
+template <int LOGP, int MODE, int FRAME, int COOP>
 __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
-    constexpr bool kLds = kPoly && (P > 1);
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLds ? kWG * kSlot : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[COOP ? kWG * kRun : 16];
 
     const uint32_t gid = blockIdx.x * kWG + threadIdx.x;
     const uint32_t group = gid >> LOGP;
@@ -93,10 +102,16 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         ooff = p.out_off[rec];
         Lout = p.out_off[rec + 1] - ooff;
     }
-    // bytes run through the keystream
-    uint64_t L = Lin;
-    if (FRAME == FR_SEAL) L = Lout;  // in || mac(out tail)
+    uint64_t L = Lin;                          // bytes run through the keystream
+    if (FRAME == FR_SEAL) L = Lout;            // in || mac (mac sits in the out tail)
+    uint64_t simple = L;                       // prefix where whole blocks take the fast path
+    if (FRAME == FR_SEAL) simple = Lin;
+    if (FRAME == FR_OPEN) simple = Lout;
     const uint32_t nb = (uint32_t)((L + 63) >> 6);
+    const uint32_t B = (nb + P - 1) >> LOGP;
+    const uint32_t cbeg = min(j * B, nb);
+    const uint32_t cend = min(cbeg + B, nb);
+    const uint32_t cfast = max(cbeg, min(cend, (uint32_t)(simple >> 6)));
     const uint8_t* __restrict__ src = p.in + ioff;
     uint8_t* __restrict__ dst = p.out + ooff;
 
@@ -120,159 +135,237 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     uint32_t ctr0 = 1;  // RFC 8439 data counter
     if (MODE == MODE_XOR) ctr0 = (p.counters && live) ? p.counters[rec] : 0u;
 
-    // ---- Poly1305 setup: one-time key from block 0, stream geometry
-    uint32_t g[5] = {0, 0, 0, 0, 0};
-    uint32_t rl[5], pad[4];
-    Pmul RP, E;
-    uint32_t na = 0, nct = 0, aad_len = 0, oj = 0;
-    uint64_t aoff = 0;
+    // ---- Poly1305: one-time key from block 0; lane 0 absorbs the AAD prefix
+    uint32_t h[5] = {0, 0, 0, 0, 0};
+    PolyR32 PR{};
+    uint32_t pad[4] = {0, 0, 0, 0};
+    uint32_t na = 0, aad_len = 0;
+    const uint32_t nct = (uint32_t)((L + 15) >> 4);
     if (kPoly) {
         uint32_t otk[16];
         chacha_block(R, 0u, otk);
-        pclamp(rl, otk[0], otk[1], otk[2], otk[3]);
+        PR = polyr32_make(otk[0], otk[1], otk[2], otk[3]);
         pad[0] = otk[4]; pad[1] = otk[5]; pad[2] = otk[6]; pad[3] = otk[7];
+        uint64_t aoff = 0;
         if (p.aad && live) {
             aoff = p.aad_off[rec];
             aad_len = (uint32_t)(p.aad_off[rec + 1] - aoff);
         }
         na = (aad_len + 15) >> 4;
-        nct = (uint32_t)((L + 15) >> 4);
-        const uint32_t N = na + nct + 1;
-        const uint32_t e = 1u + ((N - 1u - j) & (P - 1u));
-        poly_powers<LOGP>(rl, RP, E, e);
-        oj = (j - na) & (P - 1u);
-        // AAD prefix: stream blocks s < na with s == j (mod P)
-        for (uint32_t s = j; s < na; s += P) {
-            const uint8_t* ap = p.aad + aoff + 16ull * s;
-            const uint32_t cnt = min(16u, aad_len - 16u * s);
-            uint32_t w[4];
+        if (j == 0) {
+            for (uint32_t s = 0; s < na; ++s) {
+                const uint8_t* ap = p.aad + aoff + 16ull * s;
+                const uint32_t cnt = min(16u, aad_len - 16u * s);
+                uint32_t w[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                uint32_t v = 0;
+                for (int i = 0; i < 4; ++i) {
+                    uint32_t v = 0;
 #pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    if ((uint32_t)(4 * i + b) < cnt) v |= (uint32_t)ap[4 * i + b] << (8 * b);
-                w[i] = v;
+                    for (int b = 0; b < 4; ++b)
+                        if ((uint32_t)(4 * i + b) < cnt) v |= (uint32_t)ap[4 * i + b] << (8 * b);
+                    w[i] = v;
+                }
+                poly32_block(h, PR, w[0], w[1], w[2], w[3], 1u);
             }
-            pmul(g, RP);
-            padd_block(g, w[0], w[1], w[2], w[3], 1u);
         }
     }
 
-    // ---- main loop: one ChaCha20 block per lane per round
-    const uint32_t T = (nb + P - 1) >> LOGP;
-    for (uint32_t t = 0; t < T; ++t) {
-        const uint32_t c = (t << LOGP) + j;
-        const bool act = c < nb;
+    // ---- cooperative stages (uniform batches)
+    uint32_t cco = cbeg;  // first block left for the per-lane paths
+    if (COOP) {
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t wbase = threadIdx.x & ~63u;
+        const uint64_t Lu = p.uniform_len;
+        const uint32_t nfull = (uint32_t)(Lu >> 6);
+        // every lane of every record has at least fmin whole blocks (the last lane has fewest)
+        const uint32_t jl = P - 1;
+        const uint32_t fmin = (nfull > jl * B) ? min(B, nfull - jl * B) : 0u;
+        const uint32_t Ts = fmin / kStage;
+        const uint32_t kk = lane & 7u;
+        const uint32_t wgid0 = blockIdx.x * kWG + wbase;  // gid of lane 0 of this wave
+        uint64_t off[8];
+        uint32_t livemask = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t o = 8u * i + (lane >> 3);
+            const uint32_t og = (wgid0 + o) >> LOGP;
+            const uint32_t oj = (wgid0 + o) & (P - 1);
+            const uint32_t sw = (o >> 1) & 7u;
+            const bool olive = og < p.n;
+            // dead owners (last wave only) read record 0 harmlessly and never store
+            off[i] = (olive ? (uint64_t)og * Lu + 64ull * oj * B : 0ull) + 16u * (kk ^ sw);
+            livemask |= (olive ? 1u : 0u) << i;
+        }
+        const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
+        uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
+        uint8_t* wslab = slab + wbase * kRun;
+        uint8_t* myrun = slab + threadIdx.x * kRun;
+        const uint32_t msw = (lane >> 1) & 7u;
+        // prefetch registers as plain words (a uint4 array is copied with memcpy and stays
+        // in scratch)
+        uint32_t pf[32];
+        if (Ts > 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(ibase + off[i]);
+                pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+            }
+        }
+        for (uint32_t st = 0; st < Ts; ++st) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) =
+                    make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+            ENET_WAVE_LDS_SYNC();
+            uint32_t w2[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
+            }
+            {
+                // prefetch the next stage (the last iteration re-reads its own stage, an L2 hit,
+                // so the prefetch registers are written unconditionally and stay in VGPRs)
+                const uint64_t adv = (uint64_t)kRun * min(st + 1, Ts - 1);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ibase + off[i] + adv);
+                    pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                uint32_t* wb = w2 + 16 * b;
+                if (MODE == MODE_OPEN) poly_block64(h, PR, wb);
+                uint32_t ks[16];
+                chacha_block(R, ctr0 + cbeg + kStage * st + b, ks);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) wb[i] ^= ks[i];
+                if (MODE == MODE_SEAL) poly_block64(h, PR, wb);
+            }
+            if (COOP == 2) {
+                // each lane stores its own 128-byte run (8 x 16 B, per-lane addresses)
+                if (live) {
+                    uint8_t* d = dst + 64ull * (cbeg + kStage * st);
+                    store_full(d, w2);
+                    store_full(d + 64, w2 + 16);
+                }
+                ENET_WAVE_LDS_SYNC();
+            } else {
+                ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                        make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+                ENET_WAVE_LDS_SYNC();
+                const uint64_t adv = (uint64_t)kRun * st;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                    if ((livemask >> i) & 1u) *reinterpret_cast<uint4*>(obase + off[i] + adv) = v;
+                }
+                ENET_WAVE_LDS_SYNC();
+            }
+        }
+        cco = min(cfast, cbeg + kStage * Ts);
+    }
+
+    // ---- fast path: whole blocks, next block prefetched while this one is computed
+    uint32_t w[16];
+    if (cco < cfast) load_full(src + 64ull * cco, w);
+    for (uint32_t c = cco; c < cfast; ++c) {
+        uint32_t wn[16];
+        if (c + 1 < cfast) load_full(src + 64ull * (c + 1), wn);
+        if (MODE == MODE_OPEN) poly_block64(h, PR, w);
         uint32_t ks[16];
         chacha_block(R, ctr0 + c, ks);  // uint32 wrap, ChaCha20.cpp:110
-        uint32_t w[16];
-        uint32_t nbytes = 0;
-        if (act) {
-            const uint64_t pos = 64ull * c;
-            nbytes = (uint32_t)min<uint64_t>(64, L - pos);
-            if (FRAME == FR_SEAL && pos + 64 > Lin) {
-                // virtual input in[0, Lin) || out[Lin, Lout): the plaintext MAC written by the
-                // HMAC pass sits in the output record's tail
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    uint32_t v = 0;
+        for (int i = 0; i < 16; ++i) ks[i] ^= w[i];
+        store_full(dst + 64ull * c, ks);
+        if (MODE == MODE_SEAL) poly_block64(h, PR, ks);
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const uint64_t q = pos + 4 * i + b;
-                        uint32_t byte = 0;
-                        if (q < Lin) byte = src[q];
-                        else if (q < L) byte = dst[q];
-                        v |= byte << (8 * b);
-                    }
-                    w[i] = v;
+        for (int i = 0; i < 16; ++i) w[i] = wn[i];
+    }
+
+    // ---- tail: the partial block and (frames) the blocks that touch the MAC
+    for (uint32_t c = cfast; c < cend; ++c) {
+        const uint64_t pos = 64ull * c;
+        const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
+        if (FRAME == FR_SEAL && pos + 64 > Lin) {
+            // virtual input in[0, Lin) || out[Lin, Lout): the plaintext MAC written by the
+            // HMAC pass sits in the output record's tail
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint64_t q = pos + 4 * i + b;
+                    uint32_t byte = 0;
+                    if (q < Lin) byte = src[q];
+                    else if (q < L) byte = dst[q];
+                    v |= byte << (8 * b);
                 }
-            } else {
-                load_block(src + pos, nbytes, w);
+                w[i] = v;
             }
         } else {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] = 0;
+            load_block(src + pos, nbytes, w);
         }
         uint32_t o[16];
+        chacha_block(R, ctr0 + c, o);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[i] = w[i] ^ ks[i];
-        if (act) {
-            const uint64_t pos = 64ull * c;
-            if (FRAME == FR_OPEN && pos + 64 > Lout) {
-                // decrypted MAC (bytes >= Lout) goes to the tag buffer
+        for (int i = 0; i < 16; ++i) o[i] ^= w[i];
+        if (FRAME == FR_OPEN && pos + 64 > Lout) {
+            // decrypted MAC (bytes >= Lout) goes to the tag buffer
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < 16; ++i) {
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        const uint64_t q = pos + 4 * i + b;
-                        const uint8_t byte = (uint8_t)(o[i] >> (8 * b));
-                        if (q < Lout) dst[q] = byte;
-                        else if (q < L) p.tag_out[32ull * rec + (q - Lout)] = byte;
-                    }
+                for (int b = 0; b < 4; ++b) {
+                    const uint64_t q = pos + 4 * i + b;
+                    const uint8_t byte = (uint8_t)(o[i] >> (8 * b));
+                    if (q < Lout) dst[q] = byte;
+                    else if (q < L) p.tag_out[32ull * rec + (q - Lout)] = byte;
                 }
-            } else {
-                store_block(dst + pos, nbytes, o);
             }
+        } else {
+            store_block(dst + pos, nbytes, o);
         }
         if (kPoly) {
-            // ciphertext of this block, zero beyond the record (Poly1305 pads with zeros)
-            uint32_t ct[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) ct[i] = (MODE == MODE_SEAL) ? o[i] : w[i];
+            uint32_t* ct = (MODE == MODE_SEAL) ? o : w;
             if (MODE == MODE_SEAL && nbytes < 64) mask_tail(ct, nbytes);
-            const uint32_t qbase = t << (LOGP + 2);  // first ct stream block of this round
-            if (P == 1) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (qbase + u < nct) {
-                        pmul(g, RP);
-                        padd_block(g, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
-                    }
-                }
-            } else {
-                uint4* mine = reinterpret_cast<uint4*>(lds + threadIdx.x * kSlot);
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    mine[u] = make_uint4(ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3]);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t lane0 = threadIdx.x - j;  // first lane of this record's group
-                uint4 blk[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const uint32_t q = oj + P * u;  // stream block within the round
-                    blk[u] = *reinterpret_cast<const uint4*>(lds + (lane0 + (q >> 2)) * kSlot +
-                                                             (q & 3) * 16);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (qbase + oj + P * u < nct) {
-                        pmul(g, RP);
-                        padd_block(g, blk[u].x, blk[u].y, blk[u].z, blk[u].w, 1u);
-                    }
-                }
-            }
+            for (int u = 0; u < 4; ++u)
+                if (4 * c + u < nct)
+                    poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
         }
     }
 
     if (kPoly) {
-        // length block: stream index na + nct, owned by lane (na + nct) mod P
-        if (((na + nct) & (P - 1u)) == j) {
-            pmul(g, RP);
-            padd_block(g, aad_len, 0u, (uint32_t)L, (uint32_t)(L >> 32), 1u);
+        // length block LE64(|aad|) || LE64(|ct|), owned by the lane holding the last block
+        const uint32_t jlast = nb ? (nb - 1) / B : 0u;
+        const uint32_t N = na + nct + 1;
+        uint32_t e = 0;  // contribution scale: r^(N-1-s_last)
+        if (j == jlast) {
+            poly32_block(h, PR, aad_len, 0u, (uint32_t)L, (uint32_t)(L >> 32), 1u);
+        } else if (cend > cbeg) {
+            e = N - 1 - (na + 4 * cend - 1);
         }
-        pmul(g, E);
+        uint32_t l[5];
+        h32_to_limbs(h, l);
+        if (P > 1) {
+            if (e > 0) {
+                uint32_t r26[5], x[5];
+                plimbs(r26, PR.r0, PR.r1, PR.r2, PR.r3);
+                ppow(r26, e, x);
+                pmul(l, pmul_make(x));
+            }
 #pragma unroll
-        for (uint32_t off = P >> 1; off >= 1; off >>= 1) {
+            for (uint32_t off = P >> 1; off >= 1; off >>= 1) {
 #pragma unroll
-            for (int i = 0; i < 5; ++i) g[i] += __shfl_xor(g[i], (int)off);
+                for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], (int)off);
+            }
         }
         uint32_t tag[4];
-        pfinish(g, pad, tag);
+        pfinish(l, pad, tag);
         if (MODE == MODE_SEAL) {
             if (live && j == 0) {
                 uint32_t* tp = reinterpret_cast<uint32_t*>(p.tag_out + 16ull * rec);
@@ -288,7 +381,7 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
             if (live && diff != 0) {
                 // authentication failed: do not release plaintext
                 const uint32_t zero[16] = {0};
-                for (uint32_t c = j; c < nb; c += P) {
+                for (uint32_t c = cbeg; c < cend; ++c) {
                     const uint64_t pos = 64ull * c;
                     store_block(dst + pos, (uint32_t)min<uint64_t>(64, L - pos), zero);
                 }
@@ -302,7 +395,15 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     const uint64_t lanes = (uint64_t)p.n << LOGP;
     const uint32_t blocks = (uint32_t)((lanes + kWG - 1) / kWG);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((records_kernel<LOGP, MODE, FRAME>), dim3(blocks), dim3(kWG), 0, s, p);
+    if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 1)
+        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(blocks), dim3(kWG), 0,
+                           s, p);
+    else if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 2)
+        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 2>), dim3(blocks), dim3(kWG), 0,
+                           s, p);
+    else
+        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FRAME, 0>), dim3(blocks), dim3(kWG), 0,
+                           s, p);
     return hipGetLastError();
 }
 
