@@ -87,6 +87,45 @@ __device__ __forceinline__ void chacha_block(const ChachaRecord& R, uint32_t cou
     x[12] = x12 + counter; x[13] = x13 + R.n[0]; x[14] = x14 + R.n[1]; x[15] = x15 + R.n[2];
 }
 
+// Two keystream blocks of the same record, quarter-rounds interleaved (8 independent ARX
+// chains instead of 4) so a wave always has independent VALU work in flight.
+__device__ __forceinline__ void chacha_block2(const ChachaRecord& R, uint32_t ca, uint32_t cb,
+                                              uint32_t xa[16], uint32_t xb[16]) {
+    uint32_t a0 = kSigma0, a4 = R.k[0], a8 = R.k[4], a12 = ca;
+    uint32_t b0 = kSigma0, b4 = R.k[0], b8 = R.k[4], b12 = cb;
+    ENET_QR(a0, a4, a8, a12);
+    ENET_QR(b0, b4, b8, b12);
+    uint32_t a1 = R.pre[0], a5 = R.pre[1], a9 = R.pre[2], a13 = R.pre[3];
+    uint32_t a2 = R.pre[4], a6 = R.pre[5], a10 = R.pre[6], a14 = R.pre[7];
+    uint32_t a3 = R.pre[8], a7 = R.pre[9], a11 = R.pre[10], a15 = R.pre[11];
+    uint32_t b1 = a1, b5 = a5, b9 = a9, b13 = a13;
+    uint32_t b2 = a2, b6 = a6, b10 = a10, b14 = a14;
+    uint32_t b3 = a3, b7 = a7, b11 = a11, b15 = a15;
+    ENET_QR(a0, a5, a10, a15); ENET_QR(b0, b5, b10, b15);
+    ENET_QR(a1, a6, a11, a12); ENET_QR(b1, b6, b11, b12);
+    ENET_QR(a2, a7, a8, a13);  ENET_QR(b2, b7, b8, b13);
+    ENET_QR(a3, a4, a9, a14);  ENET_QR(b3, b4, b9, b14);
+#pragma unroll
+    for (int i = 1; i < 10; ++i) {
+        ENET_QR(a0, a4, a8, a12);  ENET_QR(b0, b4, b8, b12);
+        ENET_QR(a1, a5, a9, a13);  ENET_QR(b1, b5, b9, b13);
+        ENET_QR(a2, a6, a10, a14); ENET_QR(b2, b6, b10, b14);
+        ENET_QR(a3, a7, a11, a15); ENET_QR(b3, b7, b11, b15);
+        ENET_QR(a0, a5, a10, a15); ENET_QR(b0, b5, b10, b15);
+        ENET_QR(a1, a6, a11, a12); ENET_QR(b1, b6, b11, b12);
+        ENET_QR(a2, a7, a8, a13);  ENET_QR(b2, b7, b8, b13);
+        ENET_QR(a3, a4, a9, a14);  ENET_QR(b3, b4, b9, b14);
+    }
+    xa[0] = a0 + kSigma0; xa[1] = a1 + kSigma1; xa[2] = a2 + kSigma2; xa[3] = a3 + kSigma3;
+    xa[4] = a4 + R.k[0]; xa[5] = a5 + R.k[1]; xa[6] = a6 + R.k[2]; xa[7] = a7 + R.k[3];
+    xa[8] = a8 + R.k[4]; xa[9] = a9 + R.k[5]; xa[10] = a10 + R.k[6]; xa[11] = a11 + R.k[7];
+    xa[12] = a12 + ca; xa[13] = a13 + R.n[0]; xa[14] = a14 + R.n[1]; xa[15] = a15 + R.n[2];
+    xb[0] = b0 + kSigma0; xb[1] = b1 + kSigma1; xb[2] = b2 + kSigma2; xb[3] = b3 + kSigma3;
+    xb[4] = b4 + R.k[0]; xb[5] = b5 + R.k[1]; xb[6] = b6 + R.k[2]; xb[7] = b7 + R.k[3];
+    xb[8] = b8 + R.k[4]; xb[9] = b9 + R.k[5]; xb[10] = b10 + R.k[6]; xb[11] = b11 + R.k[7];
+    xb[12] = b12 + cb; xb[13] = b13 + R.n[0]; xb[14] = b14 + R.n[1]; xb[15] = b15 + R.n[2];
+}
+
 // ----------------------------------------------------------------------------- Poly1305
 // Field elements mod 2^130-5 in five 26-bit limbs.  `Pmul` holds a multiplier and its 5x
 // multiples (2^130 == 5), so h*r needs 25 v_mad_u64_u32 and a short carry chain.

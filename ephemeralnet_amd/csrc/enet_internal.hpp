@@ -34,6 +34,7 @@ struct RecParams {
     // uniform batch: every record is exactly uniform_len bytes in and out (0 = not uniform)
     uint64_t uniform_len;
     int coop;  // allow the cooperative-staging path for uniform batches
+    uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
 };
 
 // lanes: 1, 2, 4, 8 or 16 lanes per record.

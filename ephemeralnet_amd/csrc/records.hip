@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     const uint32_t group = gid >> LOGP;
     const uint32_t j = gid & (P - 1);
     const bool live = group < p.n;
-    const uint32_t rec = live ? (p.order ? p.order[group] : group) : 0u;
+    const uint32_t rec = live ? (p.order ? p.order[group] : group + p.rec_base) : 0u;
 
     // ---- record geometry
     uint64_t ioff = 0, ooff = 0, Lin = 0, Lout = 0;
@@ -184,17 +184,14 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         const uint32_t kk = lane & 7u;
         const uint32_t wgid0 = blockIdx.x * kWG + wbase;  // gid of lane 0 of this wave
         uint64_t off[8];
-        uint32_t livemask = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const uint32_t o = 8u * i + (lane >> 3);
             const uint32_t og = (wgid0 + o) >> LOGP;
             const uint32_t oj = (wgid0 + o) & (P - 1);
             const uint32_t sw = (o >> 1) & 7u;
-            const bool olive = og < p.n;
-            // dead owners (last wave only) read record 0 harmlessly and never store
-            off[i] = (olive ? (uint64_t)og * Lu + 64ull * oj * B : 0ull) + 16u * (kk ^ sw);
-            livemask |= (olive ? 1u : 0u) << i;
+            // the host launches COOP only over whole waves of live records
+            off[i] = (uint64_t)og * Lu + 64ull * oj * B + 16u * (kk ^ sw);
         }
         const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
         uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
@@ -204,68 +201,74 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         // prefetch registers as plain words (a uint4 array is copied with memcpy and stays
         // in scratch)
         uint32_t pf[32];
-        if (Ts > 0) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint4 v = *reinterpret_cast<const uint4*>(ibase + off[i]);
-                pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
-            }
-        }
-        for (uint32_t st = 0; st < Ts; ++st) {
+        auto land = [&]() {  // prefetched stage -> slab, lane-linear (whole-line layout)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) =
                     make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+        };
+        auto fetch = [&](uint32_t stage) {
+            const uint64_t adv = (uint64_t)kRun * stage;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(ibase + off[i] + adv);
+                pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+            }
+        };
+        if (Ts > 0) {
+            fetch(0);
+            land();
+        }
+        // Loop rotated so every wait on the prefetch sits after this stage's stores in the same
+        // iteration: vmcnt then waits for the (older) loads only, never for the stores.
+        for (uint32_t st = 0; st < Ts; ++st) {
             ENET_WAVE_LDS_SYNC();
+            // (b) each lane reads its own two blocks
             uint32_t w2[32];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
                 w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
             }
+            // (c) prefetch the next stage now, so its latency hides under this stage's ALU work
+            //     (the last iteration re-reads its own stage, an L2 hit, so the prefetch
+            //     registers are written unconditionally and stay in VGPRs)
+            fetch(min(st + 1, Ts - 1));
+            // keep the loads issued here: the keystream work below is made to depend on this
+            // statement, so the scheduler cannot hoist it above the loads
+            asm volatile("" : "+v"(R.k[0]) :: "memory");
+            // (d) two keystream blocks (interleaved) + Poly1305
             {
-                // prefetch the next stage (the last iteration re-reads its own stage, an L2 hit,
-                // so the prefetch registers are written unconditionally and stay in VGPRs)
-                const uint64_t adv = (uint64_t)kRun * min(st + 1, Ts - 1);
+                const uint32_t c0 = ctr0 + cbeg + kStage * st;
+                if (MODE == MODE_OPEN) {
+                    poly_block64(h, PR, w2);
+                    poly_block64(h, PR, w2 + 16);
+                }
+                uint32_t ka[16], kb[16];
+                chacha_block2(R, c0, c0 + 1, ka, kb);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(ibase + off[i] + adv);
-                    pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+                if (MODE == MODE_SEAL) {
+                    poly_block64(h, PR, w2);
+                    poly_block64(h, PR, w2 + 16);
                 }
             }
+            // (e) outputs back into the own run, (f) read lane-linear and store whole lines
+            ENET_WAVE_LDS_SYNC();
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                uint32_t* wb = w2 + 16 * b;
-                if (MODE == MODE_OPEN) poly_block64(h, PR, wb);
-                uint32_t ks[16];
-                chacha_block(R, ctr0 + cbeg + kStage * st + b, ks);
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                    make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+            ENET_WAVE_LDS_SYNC();
+            const uint64_t adv = (uint64_t)kRun * st;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) wb[i] ^= ks[i];
-                if (MODE == MODE_SEAL) poly_block64(h, PR, wb);
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                *reinterpret_cast<uint4*>(obase + off[i] + adv) = v;
             }
-            if (COOP == 2) {
-                // each lane stores its own 128-byte run (8 x 16 B, per-lane addresses)
-                if (live) {
-                    uint8_t* d = dst + 64ull * (cbeg + kStage * st);
-                    store_full(d, w2);
-                    store_full(d + 64, w2 + 16);
-                }
-                ENET_WAVE_LDS_SYNC();
-            } else {
-                ENET_WAVE_LDS_SYNC();
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
-                        make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
-                ENET_WAVE_LDS_SYNC();
-                const uint64_t adv = (uint64_t)kRun * st;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
-                    if ((livemask >> i) & 1u) *reinterpret_cast<uint4*>(obase + off[i] + adv) = v;
-                }
-                ENET_WAVE_LDS_SYNC();
-            }
+            ENET_WAVE_LDS_SYNC();
+            // (a) land the next stage in the slab
+            land();
         }
         cco = min(cfast, cbeg + kStage * Ts);
     }
@@ -395,15 +398,29 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     const uint64_t lanes = (uint64_t)p.n << LOGP;
     const uint32_t blocks = (uint32_t)((lanes + kWG - 1) / kWG);
     if (blocks == 0) return hipSuccess;
-    if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 1)
-        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(blocks), dim3(kWG), 0,
-                           s, p);
-    else if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 2)
-        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 2>), dim3(blocks), dim3(kWG), 0,
-                           s, p);
-    else
-        hipLaunchKernelGGL((records_kernel<LOGP, MODE, FRAME, 0>), dim3(blocks), dim3(kWG), 0,
-                           s, p);
+    if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 1) {
+        // cooperative kernel over whole workgroups of records (no dead owners, no store
+        // predicates); the remaining records go through the per-lane kernel
+        const uint32_t per_wg = kWG >> LOGP;
+        const uint32_t full = p.n / per_wg;
+        if (full) {
+            RecParams q = p;
+            q.n = full * per_wg;
+            hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG), 0,
+                               s, q);
+        }
+        const uint32_t rest = p.n - full * per_wg;
+        if (rest) {
+            RecParams q = p;
+            q.n = rest;
+            q.rec_base = full * per_wg;
+            hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 0>),
+                               dim3((uint32_t)((((uint64_t)rest << LOGP) + kWG - 1) / kWG)),
+                               dim3(kWG), 0, s, q);
+        }
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL((records_kernel<LOGP, MODE, FRAME, 0>), dim3(blocks), dim3(kWG), 0, s, p);
     return hipGetLastError();
 }
 
