@@ -185,7 +185,9 @@ def main():
         if os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
-            k = pmc.get("kernels", {}).get(dom)
+            lanes = E.lanes_per_record(n, n * L, L)
+            want = f"records_kernel<{lanes.bit_length() - 1}, {1 if dom == 'seal' else 2}, 0, 1>"
+            k = next((v for name, v in pmc.get("kernels", {}).items() if want in name), None)
             if k and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
                 pmc_note = os.path.relpath(PMC_FILE, ROOT)

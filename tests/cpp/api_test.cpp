@@ -1,0 +1,110 @@
+// api_test.cpp -- exercises the reference C++ API (ephemeralnet::crypto, same signatures as the
+// reference headers) exactly as a reference caller would, against libenet_crypto.so.
+// Reads one operation per line on stdin, prints one hex result per line.
+#include <cstdio>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "ephemeralnet/crypto/Batch.hpp"
+#include "ephemeralnet/crypto/ChaCha20.hpp"
+#include "ephemeralnet/crypto/CryptoManager.hpp"
+#include "ephemeralnet/crypto/HmacSha256.hpp"
+#include "ephemeralnet/crypto/Sha256.hpp"
+
+using namespace ephemeralnet;
+
+static std::vector<uint8_t> unhex(const std::string& s) {
+    std::vector<uint8_t> v;
+    if (s == "-") return v;
+    for (size_t i = 0; i + 1 < s.size(); i += 2) v.push_back((uint8_t)std::stoul(s.substr(i, 2), nullptr, 16));
+    return v;
+}
+template <class T>
+static std::string hex(const T& v) {
+    static const char* d = "0123456789abcdef";
+    std::string s;
+    for (auto b : v) { s += d[(uint8_t)b >> 4]; s += d[(uint8_t)b & 15]; }
+    return s.empty() ? "-" : s;
+}
+
+int main() {
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::istringstream in(line);
+        std::string op;
+        in >> op;
+        if (op == "chacha") {
+            std::string k, n, c, p;
+            in >> k >> n >> c >> p;
+            crypto::Key key; crypto::Nonce nonce;
+            auto kb = unhex(k), nb = unhex(n), pb = unhex(p);
+            std::copy(kb.begin(), kb.end(), key.bytes.begin());
+            std::copy(nb.begin(), nb.end(), nonce.bytes.begin());
+            std::vector<uint8_t> out;
+            crypto::ChaCha20::apply(key, nonce, pb, out, (uint32_t)std::stoul(c));
+            std::cout << hex(out) << "\n";
+        } else if (op == "sha") {
+            std::string d; in >> d;
+            std::cout << hex(crypto::Sha256::digest(unhex(d))) << "\n";
+        } else if (op == "sha_pieces") {
+            std::string pc, d; in >> pc >> d;
+            auto data = unhex(d);
+            size_t piece = std::stoul(pc);
+            crypto::Sha256 h;
+            for (size_t o = 0; o < data.size(); o += piece)
+                h.update(std::span<const uint8_t>(data.data() + o, std::min(piece, data.size() - o)));
+            std::cout << hex(h.finalize()) << "\n";
+        } else if (op == "hmac") {
+            std::string k, d; in >> k >> d;
+            std::cout << hex(crypto::HmacSha256::compute(unhex(k), unhex(d))) << "\n";
+        } else if (op == "hverify") {
+            std::string k, d, m; in >> k >> d >> m;
+            std::cout << (crypto::HmacSha256::verify(unhex(k), unhex(d), unhex(m)) ? "1" : "0") << "\n";
+        } else if (op == "cm_dec") {
+            std::string k, id, n, c; in >> k >> id >> n >> c;
+            crypto::Key key; crypto::Nonce nonce; ChunkId cid;
+            auto kb = unhex(k), ib = unhex(id), nb = unhex(n);
+            std::copy(kb.begin(), kb.end(), key.bytes.begin());
+            std::copy(ib.begin(), ib.end(), cid.begin());
+            std::copy(nb.begin(), nb.end(), nonce.bytes.begin());
+            auto pt = crypto::CryptoManager::decrypt_with_key(key, cid, unhex(c), nonce);
+            std::cout << hex(*pt) << "\n";
+        } else if (op == "cm_roundtrip") {
+            std::string id, p; in >> id >> p;
+            ChunkId cid; auto ib = unhex(id);
+            std::copy(ib.begin(), ib.end(), cid.begin());
+            auto key = crypto::CryptoManager::generate_key();
+            ChunkData pt = unhex(p);
+            auto ct = crypto::CryptoManager::encrypt_with_key(key, cid, pt);
+            auto back = crypto::CryptoManager::decrypt_with_key(key, cid, ct.data, ct.nonce);
+            std::cout << ((back && *back == pt && (pt.empty() || ct.data != pt)) ? "1" : "0") << "\n";
+        } else if (op == "frame_seal") {
+            std::string k, n, m; in >> k >> n >> m;
+            std::array<uint8_t, 32> key{}; crypto::Nonce nonce;
+            auto kb = unhex(k), nb = unhex(n);
+            std::copy(kb.begin(), kb.end(), key.begin());
+            std::copy(nb.begin(), nb.end(), nonce.bytes.begin());
+            auto mb = unhex(m);
+            std::span<const uint8_t> ms[1] = {mb};
+            auto bodies = crypto::batch::frame_seal(std::span(&key, 1), std::span(&nonce, 1), ms);
+            std::vector<uint8_t> ok;
+            std::span<const uint8_t> bs[1] = {bodies[0]};
+            auto back = crypto::batch::frame_open(std::span(&key, 1), std::span(&nonce, 1), bs, ok);
+            std::cout << hex(bodies[0]) << " " << (ok[0] == 1 && back[0] == mb ? "1" : "0") << "\n";
+        } else if (op == "aead_seal") {
+            std::string k, n, p; in >> k >> n >> p;
+            crypto::Key key; crypto::Nonce nonce;
+            auto kb = unhex(k), nb = unhex(n), pb = unhex(p);
+            std::copy(kb.begin(), kb.end(), key.bytes.begin());
+            std::copy(nb.begin(), nb.end(), nonce.bytes.begin());
+            std::span<const uint8_t> ps[1] = {pb};
+            auto s = crypto::batch::aead_seal(std::span(&key, 1), std::span(&nonce, 1), ps);
+            std::cout << hex(s[0].data) << " " << hex(s[0].tag) << "\n";
+        } else if (!op.empty()) {
+            std::cout << "?\n";
+        }
+    }
+    return 0;
+}
