@@ -141,7 +141,8 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     uint32_t pad[4] = {0, 0, 0, 0};
     uint32_t na = 0, aad_len = 0;
     const uint32_t nct = (uint32_t)((L + 15) >> 4);
-    if (kPoly) {
+    auto poly_setup = [&]() {
+        if (!kPoly) return;
         uint32_t otk[16];
         chacha_block(R, 0u, otk);
         PR = polyr32_make(otk[0], otk[1], otk[2], otk[3]);
@@ -168,7 +169,8 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
                 poly32_block(h, PR, w[0], w[1], w[2], w[3], 1u);
             }
         }
-    }
+    };
+    if (!COOP) poly_setup();
 
     // ---- cooperative stages (uniform batches)
     uint32_t cco = cbeg;  // first block left for the per-lane paths
@@ -215,10 +217,9 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
                 pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
             }
         };
-        if (Ts > 0) {
-            fetch(0);
-            land();
-        }
+        if (Ts > 0) fetch(0);
+        poly_setup();  // the one-time-key block runs while the first stage is in flight
+        if (Ts > 0) land();
         // Loop rotated so every wait on the prefetch sits after this stage's stores in the same
         // iteration: vmcnt then waits for the (older) loads only, never for the stores.
         for (uint32_t st = 0; st < Ts; ++st) {

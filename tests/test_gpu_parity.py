@@ -340,3 +340,43 @@ def test_frames_random_vs_oracle(enet, lanes):
     bodies = records_of(host(out), ooffs.tolist())
     for i in range(n):
         assert bodies[i] == oracle.frame_seal(keys[i], nonces[i], msgs[i]), i
+
+
+# ------------------------------------------------------------------------------ uniform (COOP)
+@pytest.mark.parametrize("L,n,lanes", [(1500, 1000, 1), (1500, 517, 2), (4096, 300, 2),
+                                       (4096, 129, 4), (65536, 40, 8), (65536, 33, 16),
+                                       (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1)])
+def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes):
+    """Uniform-length batches take the cooperative LDS-staged path (whole workgroups) plus the
+    per-lane path for the partial workgroup; 1500-byte records start unaligned and end in a
+    partial block."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    items = [splitmix_bytes(70000 + i, L) for i in range(n)]
+    keys = [splitmix_bytes(80000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(90000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces)
+    assert b.total_bytes_hint == n * L and b.max_len_hint == L
+    out = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    got = records_of(host(out), b.offsets.cpu().tolist())
+    th = host(tags)
+    idx = range(n) if n * max(L, 1) <= 4 << 20 else np.linspace(0, n - 1, 64).astype(int)
+    for i in idx:
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct, (i, L)
+        assert th[16 * i:16 * i + 16] == tag, (i, L)
+    b2 = enet.Batch(out, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    back = torch.zeros_like(out)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, back, tags, ok)
+    assert int(ok.sum()) == n
+    assert torch.equal(back, b.arena)
+    # xor mode (reference ChaCha20::apply with per-record counters) on the same shape
+    ctr = np.frombuffer(splitmix_bytes(L + n, 4 * n), dtype="<u4").copy()
+    xo = out_like(b)
+    enet.chacha20_xor(b, xo, counters=torch.tensor(ctr.view(np.int32)).cuda())
+    xg = records_of(host(xo), b.offsets.cpu().tolist())
+    for i in list(idx)[:64]:
+        assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i]))
