@@ -33,8 +33,9 @@ PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r01.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed steps; MI355X clocks ramp over the first ~10 ms of sustained load")
     ap.add_argument("--records", type=int, default=65536)
     ap.add_argument("--record-bytes", type=int, default=4096)
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per record (0 = scheduler)")
@@ -45,6 +46,9 @@ def parse():
                     help="host-resident path: pinned host buffers, H2D -> kernel -> D2H pipelined "
                          "over 3 streams in 16 MiB chunks (recorded in DESIGN.md, never `value`)")
     ap.add_argument("--chunk-records", type=int, default=4096)
+    ap.add_argument("--c5", action="store_true",
+                    help="SURVEY 8d C5: log-uniform 512 B-64 KiB records, AEAD + fused HMAC-SHA256, "
+                         "host-resident (H2D + kernels + D2H), records per GPU = --records")
     ap.add_argument("--mode", default="aead", choices=["aead", "xor"],
                     help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline probe)")
     return ap.parse_args()
@@ -171,8 +175,127 @@ def e2e(args) -> dict:
     }
 
 
+def c5(args) -> dict:
+    """Mixed-size batch with the fused HMAC-SHA256 tag, starting and ending in pinned host
+    memory.  Chunks of ~64 MiB go H2D -> aead_hmac_seal -> D2H (then the open direction) on 3
+    streams; inside a chunk records are processed longest-first (`order`) so waves stay balanced.
+    Multi-GPU: each rank takes a byte-balanced contiguous share (shard.py), no collective."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ephemeralnet_amd as E
+    from ephemeralnet_amd.shard import shard_ranges
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    rng = np.random.default_rng(5)
+    n_all = args.records * world
+    lens_all = np.exp(rng.uniform(np.log(512), np.log(65536), n_all)).astype(np.int64)
+    lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
+    lens = lens_all[lo:hi]
+    n = len(lens)
+    offs_h = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    total = int(offs_h[-1])
+    g = torch.Generator().manual_seed(11 + rank)
+    pt_h = torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g).pin_memory()
+    ct_h = torch.empty_like(pt_h).pin_memory()
+    back_h = torch.empty_like(pt_h).pin_memory()
+    nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
+    tags_h = torch.empty(16 * n, dtype=torch.uint8).pin_memory()
+    macs_h = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
+    ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev)
+    # chunks of ~64 MiB on record boundaries
+    target = 64 << 20
+    cuts = [0]
+    while cuts[-1] < n:
+        k = int(np.searchsorted(offs_h, offs_h[cuts[-1]] + target, side="left"))
+        cuts.append(max(cuts[-1] + 1, min(k, n)))
+    chunks = []
+    for c0, c1 in zip(cuts[:-1], cuts[1:]):
+        o = offs_h[c0:c1 + 1] - offs_h[c0]
+        order = np.argsort(-lens[c0:c1], kind="stable").astype(np.int32)
+        chunks.append((c0, c1, torch.tensor(o, device=dev), torch.tensor(order, device=dev),
+                       int(o[-1]), int(lens[c0:c1].max())))
+    S = 3
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    cap = max(c[4] for c in chunks)
+    mrec = max(c[1] - c[0] for c in chunks)
+    din = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(S)]
+    dout = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(S)]
+    dn = [torch.empty(12 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
+    dt = [torch.empty(16 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
+    dm = [torch.empty(32 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
+    dok = [torch.empty(mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
+
+    def run(kind):
+        for ci, (c0, c1, o, order, nbytes, mx) in enumerate(chunks):
+            s = ci % S
+            st = streams[s]
+            b0, b1 = int(offs_h[c0]), int(offs_h[c1])
+            m = c1 - c0
+            with torch.cuda.stream(st):
+                din[s][:nbytes].copy_((pt_h if kind == "seal" else ct_h)[b0:b1], non_blocking=True)
+                dn[s][:12 * m].copy_(nonces_h[12 * c0:12 * c1], non_blocking=True)
+                bt = E.Batch(din[s], o, keys[32 * c0:32 * c1], dn[s], order=order,
+                             total_bytes_hint=nbytes, max_len_hint=mx)
+                if kind == "seal":
+                    E.aead_hmac_seal(bt, dout[s], dt[s], dm[s], stream=st)
+                    ct_h[b0:b1].copy_(dout[s][:nbytes], non_blocking=True)
+                    tags_h[16 * c0:16 * c1].copy_(dt[s][:16 * m], non_blocking=True)
+                    macs_h[32 * c0:32 * c1].copy_(dm[s][:32 * m], non_blocking=True)
+                else:
+                    dt[s][:16 * m].copy_(tags_h[16 * c0:16 * c1], non_blocking=True)
+                    dm[s][:32 * m].copy_(macs_h[32 * c0:32 * c1], non_blocking=True)
+                    E.aead_hmac_open(bt, dout[s], dt[s], dm[s], dok[s], stream=st)
+                    back_h[b0:b1].copy_(dout[s][:nbytes], non_blocking=True)
+                    ok_h[c0:c1].copy_(dok[s][:m], non_blocking=True)
+        torch.cuda.synchronize(dev)
+
+    run("seal")
+    run("open")
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    run("seal")
+    run("open")
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    assert int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
+    res = None
+    if rank == 0:
+        res = {
+            "metric": "GiB/s AEAD + fused HMAC-SHA256 seal+open, mixed 512 B-64 KiB, "
+                      "host-resident (H2D + kernels + D2H)",
+            "value": round(int(lens_all.sum()) / el / 2**30, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "config": {"workload": "C5", "records_total": n_all, "bytes_total": int(lens_all.sum()),
+                       "chunk_bytes": target, "streams": S, "host_buffers": "pinned"},
+        }
+    if world > 1:
+        dist.destroy_process_group()
+    return res
+
+
 def main():
     args = parse()
+    if args.c5:
+        r = c5(args)
+        if r:
+            print(json.dumps(r), flush=True)
+        return
     if args.e2e:
         print(json.dumps(e2e(args)), flush=True)
         return

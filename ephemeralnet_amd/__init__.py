@@ -48,7 +48,8 @@ class _Records(C.Structure):
 EXPORTS = [
     "enet_chacha20_xor_batch", "enet_aead_seal_batch", "enet_aead_open_batch",
     "enet_sha256_batch", "enet_hmac_sha256_batch", "enet_hmac_sha256_verify_batch",
-    "enet_frame_seal_batch", "enet_frame_open_batch", "enet_chunk_counter",
+    "enet_frame_seal_batch", "enet_frame_open_batch", "enet_aead_hmac_seal_batch",
+    "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_last_error", "enet_abi_version",
 ]
 
@@ -73,6 +74,8 @@ def lib() -> C.CDLL:
         L.enet_hmac_sha256_verify_batch.argtypes = [u32, vp, vp, u32, vp, vp, vp, vp, vp]
         L.enet_frame_seal_batch.argtypes = [rp, vp]
         L.enet_frame_open_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_aead_hmac_seal_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_aead_hmac_open_batch.argtypes = [rp, vp, vp, vp, vp]
         L.enet_chunk_counter.argtypes = [C.c_char_p]
         L.enet_chunk_counter.restype = u32
         L.enet_lanes_per_record.argtypes = [u32, u64, u32]
@@ -159,6 +162,19 @@ def aead_open(b: Batch, out, tags, ok, aad=None, aad_offsets=None, stream=None) 
     r = b.records(out, b.offsets)
     _check(lib().enet_aead_open_batch(C.byref(r), _ptr(aad), _ptr(aad_offsets), _ptr(tags),
                                       _ptr(ok), _stream(stream)), "enet_aead_open_batch")
+
+
+def aead_hmac_seal(b: Batch, out, tags, macs, stream=None) -> None:
+    """AEAD seal + HMAC-SHA256(key_i, plaintext_i)."""
+    r = b.records(out, b.offsets)
+    _check(lib().enet_aead_hmac_seal_batch(C.byref(r), _ptr(tags), _ptr(macs), _stream(stream)),
+           "enet_aead_hmac_seal_batch")
+
+
+def aead_hmac_open(b: Batch, out, tags, macs, ok, stream=None) -> None:
+    r = b.records(out, b.offsets)
+    _check(lib().enet_aead_hmac_open_batch(C.byref(r), _ptr(tags), _ptr(macs), _ptr(ok),
+                                           _stream(stream)), "enet_aead_hmac_open_batch")
 
 
 def sha256(arena, offsets, digests, stream=None) -> None:

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -82,8 +83,10 @@ namespace enet {
 static std::atomic<uint32_t> g_forced_lanes{0};
 
 // Give each record enough lanes that the grid holds >= ENET_TARGET_LANES lanes
-// (default 2 waves per SIMD on 256 CUs = 131072) without giving a record more lanes than it
-// has 64-byte blocks.  ENET_LANES forces a value (tuning / tests).
+// (default 2 waves per SIMD on 256 CUs = 131072), but keep >= 8 ChaCha20 blocks per lane: every
+// lane pays one one-time-key block and, for P > 1, one r^e power, so thinner lanes lose more to
+// that fixed cost than they gain in occupancy.  ENET_LANES / enet_set_lanes_per_record force a
+// value (tuning / tests).
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len) {
     static const uint32_t forced = [] {
         const char* s = std::getenv("ENET_LANES");
@@ -96,11 +99,11 @@ uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len) {
     if (uint32_t f = g_forced_lanes.load(std::memory_order_relaxed)) return f;
     if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16) return forced;
     if (n == 0) return 1;
-    uint64_t blocks_cap = kMaxLanesPerRecord;
-    uint64_t typical = max_len ? max_len : (total_bytes ? total_bytes / n : 0);
-    if (typical) blocks_cap = (typical + 63) / 64;
+    uint64_t cap = kMaxLanesPerRecord;
+    const uint64_t typical = total_bytes ? total_bytes / n : max_len;
+    if (typical) cap = std::max<uint64_t>(1, ((typical + 63) / 64) / 8);
     uint32_t lanes = 1;
-    while (lanes < kMaxLanesPerRecord && (uint64_t)n * lanes < target && lanes * 2 <= blocks_cap)
+    while (lanes < kMaxLanesPerRecord && (uint64_t)n * lanes < target && lanes * 2 <= cap)
         lanes *= 2;
     return lanes;
 }
@@ -219,6 +222,56 @@ int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, const uint64_
     p.expect = macs;
     p.ok = ok;
     return hip_status(enet::launch_sha(p, (hipStream_t)stream), "hmac verify launch");
+}
+
+int enet_aead_hmac_seal_batch(const enet_records* r, uint8_t* tags, uint8_t* macs,
+                              void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!tags || !aligned4(tags) || !macs) return fail(ENET_EINVAL, "tags/macs NULL or misaligned");
+    hipStream_t st = (hipStream_t)stream;
+    // HMAC over the plaintext (encode_signed semantics), then the AEAD pass
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->in;
+    s.off = r->in_offsets;
+    s.digest = macs;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.order = r->order;
+    if (int e = hip_status(enet::launch_sha(s, st), "aead_hmac_seal hmac")) return e;
+    enet::RecParams p = rec_params(r);
+    p.tag_out = tags;
+    return hip_status(enet::launch_records(enet::MODE_SEAL, p, lanes_for(r), st),
+                      "aead_hmac_seal aead");
+}
+
+int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags, const uint8_t* macs,
+                              uint8_t* ok, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!tags || !aligned4(tags) || !macs || !ok)
+        return fail(ENET_EINVAL, "tags/macs/ok NULL or misaligned");
+    hipStream_t st = (hipStream_t)stream;
+    enet::RecParams p = rec_params(r);
+    p.tag_in = tags;
+    p.ok = ok;
+    if (int e = hip_status(enet::launch_records(enet::MODE_OPEN, p, lanes_for(r), st),
+                           "aead_hmac_open aead"))
+        return e;
+    // HMAC verify over the decrypted plaintext, AND-ed into ok; zero the record on failure
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->out;
+    s.off = r->out_offsets;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.expect = macs;
+    s.ok = ok;
+    s.and_ok = 1;
+    s.zero_on_fail = r->out;
+    s.order = r->order;
+    return hip_status(enet::launch_sha(s, st), "aead_hmac_open hmac verify");
 }
 
 int enet_frame_seal_batch(const enet_records* r, void* stream) {

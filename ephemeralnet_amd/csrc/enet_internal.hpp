@@ -54,6 +54,7 @@ struct ShaParams {
     uint8_t* ok;               // verify verdicts
     const uint64_t* guard_off; // verify: records whose guard length is < 32 fail (Message.cpp:315)
     uint8_t* zero_on_fail;     // verify: arena (indexed like `in`) to zero for failed records
+    int and_ok;                // verify: ok[i] &= (mac matches) instead of ok[i] = ...
     const uint32_t* order;     // nullable
 };
 hipError_t launch_sha(const ShaParams& p, hipStream_t s);

@@ -137,6 +137,7 @@ __global__ __launch_bounds__(kWG) void sha_kernel(ShaParams p) {
             diff |= ev ^ st[i];
         }
         if (p.guard_off && (p.guard_off[rec + 1] - p.guard_off[rec]) < 32) diff = 1;
+        if (p.and_ok && p.ok[rec] == 0) diff |= 1;  // fused with an earlier check (AEAD tag)
         p.ok[rec] = diff == 0 ? 1 : 0;
         if (diff != 0 && p.zero_on_fail) {
             uint8_t* z = p.zero_on_fail + off;

@@ -50,9 +50,10 @@ typedef struct enet_records {
     const uint8_t* keys;        /* [n][32] ChaCha20 keys, or [1][32] when key_stride == 0 */
     uint32_t key_stride;        /* 32 = per-record key (per-peer sessions), 0 = one shared key */
     const uint8_t* nonces;      /* [n][12] 96-bit nonces */
-    const uint32_t* order;      /* optional [n] processing order (e.g. records sorted by length,
-                                   longest first); NULL = 0..n-1.  Results are position-indexed
-                                   either way. */
+    const uint32_t* order;      /* optional [count] record indices to process, in this order
+                                   (e.g. longest first, or one length class of a larger batch);
+                                   NULL = 0..count-1.  Indices address offsets/keys/nonces/tags/ok
+                                   of the full batch, so results stay position-indexed. */
     uint64_t total_bytes_hint;  /* host-known sum of input lengths, 0 = unknown (scheduling) */
     uint32_t max_len_hint;      /* host-known max record length, 0 = unknown (scheduling) */
 } enet_records;
@@ -107,6 +108,18 @@ ENET_API int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, cons
  *       header nonce || BE32(len) (SessionManager.cpp:376-387) is host framing. */
 ENET_API int enet_frame_seal_batch(const enet_records* r, void* stream);
 ENET_API int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
+
+/* ---- AEAD with a fused HMAC-SHA256 integrity tag ("AEAD plus fused
+ *      HMAC-SHA256 tag and verify").  The HMAC covers the plaintext under the record's 32-byte
+ *      key, exactly what the reference signs before encrypting (encode_signed,
+ *      src/protocol/Message.cpp:305-311, HmacSha256.cpp:11-39).
+ * seal: out_i = ChaCha20-Poly1305 ciphertext, tags[i] = Poly1305 tag, macs[i] = HMAC_K(pt_i).
+ * open: out_i = plaintext, ok[i] = Poly1305 tag verified AND HMAC verified (HmacSha256.cpp:41-54);
+ *       on failure out_i is zeroed. */
+ENET_API int enet_aead_hmac_seal_batch(const enet_records* r, uint8_t* tags, uint8_t* macs,
+                                       void* stream);
+ENET_API int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags,
+                                       const uint8_t* macs, uint8_t* ok, void* stream);
 
 /* ---- helpers (host) */
 /* LE32(chunk_id[0..3]) -- CryptoManager.cpp:8-13 derive_counter. */

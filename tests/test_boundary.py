@@ -73,9 +73,12 @@ def test_library_loads_and_host_helpers(built):
     assert E.chunk_counter(bytes([1, 2, 3, 4]) + bytes(28)) == 0x04030201
     # scheduler: many records -> 1 lane, few large records -> more lanes, capped by blocks
     assert E.lanes_per_record(1 << 20, (1 << 20) * 1500, 1500) == 1
-    assert E.lanes_per_record(65536, 65536 * 4096, 4096) in (2, 4)
+    assert E.lanes_per_record(65536, 65536 * 4096, 4096) == 2        # C2
+    assert E.lanes_per_record(1 << 20, (1 << 20) * 1500, 1500) == 1  # C3
+    assert E.lanes_per_record(32768, 32768 * 65536, 65536) == 4      # C4 per GPU
     assert E.lanes_per_record(64, 64 * 65536, 65536) == 16
     assert E.lanes_per_record(64, 64 * 64, 64) == 1
+    assert E.lanes_per_record(100000, 100000 * 512, 512) == 1        # >= 8 blocks per lane
     with pytest.raises(E.EnetError):
         E.set_lanes_per_record(3)
     E.set_lanes_per_record(0)

@@ -380,3 +380,72 @@ def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes):
     xg = records_of(host(xo), b.offsets.cpu().tolist())
     for i in list(idx)[:64]:
         assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i]))
+
+
+# ------------------------------------------------------------------------------ AEAD + HMAC (C5)
+@pytest.mark.parametrize("lanes", [0, 1, 4])
+def test_aead_hmac_mixed_vs_oracle(enet, lanes):
+    """Mixed 512 B - 64 KiB records (log-uniform, C5 shape, small n): Poly1305 tag and
+    HMAC-SHA256(key, plaintext) bit-exact; open verifies both and rejects either tampering."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 64
+    rng = np.random.default_rng(123)
+    lens = np.exp(rng.uniform(np.log(512), np.log(65536), n)).astype(int).tolist()
+    items = [splitmix_bytes(110000 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(120000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(130000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces)
+    out = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    macs = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_hmac_seal(b, out, tags, macs)
+    offs = b.offsets.cpu().tolist()
+    got, th, mh = records_of(host(out), offs), host(tags), host(macs)
+    for i in range(n):
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct and th[16 * i:16 * i + 16] == tag, i
+        assert mh[32 * i:32 * i + 32] == oracle.hmac_sha256(keys[i], items[i]), i
+    ct2 = out.clone()
+    macs2 = macs.clone()
+    ct2[offs[5] + 3] ^= 1        # poly1305 must reject record 5
+    macs2[32 * 9 + 7] ^= 2       # hmac must reject record 9
+    b2 = enet.Batch(ct2, b.offsets, b.keys, b.nonces, total_bytes_hint=b.total_bytes_hint,
+                    max_len_hint=b.max_len_hint)
+    back = torch.full_like(out, 0x55)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_hmac_open(b2, back, tags, macs2, ok)
+    okh = ok.cpu().tolist()
+    bk = records_of(host(back), offs)
+    for i in range(n):
+        if i in (5, 9):
+            assert okh[i] == 0 and bk[i] == bytes(len(bk[i]))
+        else:
+            assert okh[i] == 1 and bk[i] == items[i], i
+
+
+def test_c1_single_key_gpu_cpu_roundtrips(enet):
+    """1024 x 4 KiB, one session key (key_stride 0), per-record nonces.  GPU seal ->
+    CPU (oracle) open, CPU seal -> GPU open, and the reference-mode ChaCha20 both ways."""
+    import torch
+    enet.set_lanes_per_record(0)
+    n, L = 1024, 4096
+    key = splitmix_bytes(1, 32)
+    items = [splitmix_bytes(140000 + i, L) for i in range(n)]
+    nonces = [splitmix_bytes(150000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, [key], nonces, key_stride=0)
+    ct = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, ct, tags)
+    cth, th = records_of(host(ct), b.offsets.cpu().tolist()), host(tags)
+    for i in range(0, n, 7):
+        ok, pt = oracle.aead_open(key, nonces[i], cth[i], th[16 * i:16 * i + 16])
+        assert ok and pt == items[i]
+    # CPU seal -> GPU open
+    sealed = [oracle.aead_seal(key, nonces[i], items[i]) for i in range(n)]
+    bo = enet.make_batch([s[0] for s in sealed], [key], nonces, key_stride=0)
+    t2 = dev(b"".join(s[1] for s in sealed))
+    back = out_like(bo)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(bo, back, t2, ok)
+    assert int(ok.sum()) == n and torch.equal(back, b.arena)
