@@ -58,16 +58,24 @@ def main():
             print(f"pass {tag} failed rc={rc}", file=sys.stderr)
             sys.exit(rc)
         for f in glob.glob(os.path.join(a.out, "**", f"{tag}_counter_collection.csv"), recursive=True):
+            seen = set()
             for row in csv.DictReader(open(f)):
                 k = kernel_key(row["Kernel_Name"])
                 if k:
                     vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    did = (row["Dispatch_Id"], tag)
+                    if did not in seen:
+                        seen.add(did)
+                        dur = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
+                        vals[k][f"dur_ns_{tag}"].append(float(dur))
     summary = {"config": json.loads(a.config) if a.config else None, "kernels": {}}
     for k, d in vals.items():
         m = {c: sum(v) / len(v) for c, v in d.items()}
         out = dict(m)
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
             out["hbm_bytes_per_launch"] = (2 * m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024
+        if "GRBM_GUI_ACTIVE" in m and "dur_ns_p0" in m:
+            out["eff_clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8.0 / m["dur_ns_p0"]
         if "GRBM_GUI_ACTIVE" in m and "SQ_ACTIVE_INST_VALU" in m:
             cyc = m["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
             # ACTIVE_INST_VALU counts quad-cycles of VALU issue summed over SIMDs
