@@ -25,7 +25,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-VALU_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 ops/s (same table)
+# int32 VALU: one wave64 instruction per 4 cycles per SIMD (measured: SQ_ACTIVE_INST_VALU equals
+# SQ_INSTS_VALU in quad-cycles, tools/ubench.hip) -> 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
+VALU_PEAK_TOPS = 39.3
+WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r01.json")
 
@@ -94,10 +97,16 @@ def cpu_baseline(record_bytes: int, budget_s: float) -> dict:
         reps += 1
         if time.perf_counter() - t_start > budget_s or reps >= 64:
             break
+    # the same kernel on one core (SURVEY.md 8d asks for both numbers)
+    n1 = min(n, max(64, (64 << 20) // max(L, 1) // 8))
+    fails = lib.orc_bench_aead(p(pt), p(ct), p(back), p(keys), p(nonces), p(tags), n1, L, 1, secs)
+    assert fails == 0
+    one_core = n1 * L / (secs[0] + secs[1]) / 2**30
     return {
         "value": round(total_b / total_s / 2**30, 4),
         "unit": "GiB/s",
         "cores": threads,
+        "one_core_value": round(one_core, 4),
         "kind": "port",
         "sample": f"{reps} x {n} records x {L} B AEAD seal+open (oracle/enet_oracle.c, "
                   f"byte-wise like src/crypto/ChaCha20.cpp, -O2), {threads} threads",
@@ -394,6 +403,7 @@ def main():
         dom_gbs = seal_gbs if dom == "seal" else open_gbs
         traffic = None
         pmc_note = None
+        valu = None
         if os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
@@ -403,6 +413,20 @@ def main():
             if k and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
                 pmc_note = os.path.relpath(PMC_FILE, ROOT)
+                if "SQ_INSTS_VALU" in k:
+                    # lane-ops per launch from the PMC instruction count, over the kernel time
+                    # measured live above
+                    ops = k["SQ_INSTS_VALU"] * 64
+                    dom_s = (seal_ms if dom == "seal" else open_ms) * 1e-3
+                    valu = {
+                        "achieved": round(ops / dom_s / 1e12, 2),
+                        "peak": VALU_PEAK_TOPS,
+                        "unit": "T int32 lane-ops/s",
+                        "frac": round(ops / dom_s / 1e12 / VALU_PEAK_TOPS, 4),
+                        "valu_busy_pmc": round(k.get("valu_busy_frac", 0.0), 4),
+                        "ops_per_64B_block": round(ops / (n * L / 64), 1),
+                        "source": pmc_note,
+                    }
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -417,7 +441,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic (torch.randint on device; random per-record keys and nonces)",
             "config": {
-                "workload": f"C2: {n} x {L} B records, per-record (key, nonce), AEAD seal+open, "
+                "workload": f"{WORKLOADS.get((n, L), 'custom')}: {n} x {L} B records, per-record (key, nonce), AEAD seal+open, "
                             "device-resident",
                 "records_per_gpu": n,
                 "record_bytes": L,
@@ -426,6 +450,8 @@ def main():
             },
             "seal_ms": round(seal_ms, 4),
             "open_ms": round(open_ms, 4),
+            "seal_gibs": round(n * L / (seal_ms * 1e-3) / 2**30, 1),
+            "open_gibs": round(n * L / (open_ms * 1e-3) / 2**30, 1),
             "roofline": {
                 "bound": "hbm",
                 "kernel": f"records_kernel ({dom})",
@@ -436,8 +462,9 @@ def main():
                 "traffic": traffic,
                 "traffic_source": pmc_note,
                 "algorithmic_bytes_per_launch": seal_bytes if dom == "seal" else open_bytes,
-                "note": "int32 VALU-bound in practice (~20 ops/B per pass), see DESIGN.md",
+                "note": "int32 VALU-bound in practice (~18 ops/B per pass): see valu_roofline",
             },
+            "valu_roofline": valu,
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
