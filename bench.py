@@ -30,6 +30,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 VALU_PEAK_TOPS = 39.3
 WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
+MODE_DESC = {"aead": "AEAD seal+open", "xor": "ChaCha20 xor twice",
+             "wire": "wire frames (nonce||BE32||ChaCha20(m||HMAC)) seal+open",
+             "store": "chunk store (SHA-256 id + ChaCha20) + fetch (decrypt + SHA-256 check)"}
+METRICS = {  # the headline is `aead`; the others are SURVEY 8d/8f side measurements
+    "aead": METRIC,
+    "xor": "GiB/s ChaCha20 xor pass pair (device-resident)",
+    "wire": "GiB/s session wire frames seal+open (device-resident)",
+    "store": "GiB/s chunk store+fetch pipeline, SHA-256 + ChaCha20 (device-resident)",
+}
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r01.json")
 
 
@@ -52,8 +61,10 @@ def parse():
     ap.add_argument("--c5", action="store_true",
                     help="SURVEY 8d C5: log-uniform 512 B-64 KiB records, AEAD + fused HMAC-SHA256, "
                          "host-resident (H2D + kernels + D2H), records per GPU = --records")
-    ap.add_argument("--mode", default="aead", choices=["aead", "xor"],
-                    help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline probe)")
+    ap.add_argument("--mode", default="aead", choices=["aead", "xor", "wire", "store"],
+                    help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline "
+                         "probe); wire = session wire frames seal+open (SURVEY 8f row 1, messages "
+                         "of --record-bytes); store = chunk store+fetch pipeline (8f row 2)")
     return ap.parse_args()
 
 
@@ -337,16 +348,32 @@ def main():
     seal_b = E.Batch(pt, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
     open_b = E.Batch(ct, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
     stream = torch.cuda.current_stream(dev)
+    if args.mode == "wire":
+        F = L + 48  # nonce(12) || BE32 || m || HMAC(32)
+        foffs = torch.arange(0, (n + 1) * F, F, dtype=torch.int64, device=dev)
+        frames = torch.empty(n * F, dtype=torch.uint8, device=dev)
+        macs = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+        wire_b = E.Batch(frames, foffs, keys, None, total_bytes_hint=n * F, max_len_hint=F)
+    if args.mode == "store":
+        hashes = torch.empty(32 * n, dtype=torch.uint8, device=dev)
 
     def seal():
         if args.mode == "aead":
             E.aead_seal(seal_b, ct, tags, stream=stream)
+        elif args.mode == "wire":
+            E.wire_seal(seal_b, frames, foffs, stream=stream)
+        elif args.mode == "store":
+            E.chunk_store(seal_b, ct, hashes, stream=stream)
         else:
             E.chacha20_xor(seal_b, ct, stream=stream)
 
     def open_():
         if args.mode == "aead":
             E.aead_open(open_b, back, tags, ok, stream=stream)
+        elif args.mode == "wire":
+            E.wire_open(wire_b, back, offs, macs, ok, stream=stream)
+        elif args.mode == "store":
+            E.chunk_fetch(open_b, back, hashes, hashes, ok, stream=stream)
         else:
             E.chacha20_xor(open_b, back, stream=stream)
 
@@ -387,7 +414,7 @@ def main():
     reps = max(4, args.steps)
     seal_ms = kernel_ms(seal, reps)
     open_ms = kernel_ms(open_, reps)
-    okh = int(ok.sum().item()) if args.mode == "aead" else n
+    okh = int(ok.sum().item()) if args.mode != "xor" else n
     if okh != n:
         raise SystemExit(f"rank {rank}: {n - okh} records failed to open")
 
@@ -395,8 +422,9 @@ def main():
         total_bytes = n * L * args.steps * world
         value = total_bytes / elapsed / 2**30
         # algorithmic HBM bytes per launch: seal 2L+64, open 2L+65 per record
-        seal_bytes = n * (2 * L + 64)
-        open_bytes = n * (2 * L + 65)
+        # (xor: 2L + key/nonce/counter 48; wire: frames carry 48 more bytes; store: hashes/ids)
+        seal_bytes = n * (2 * L + {"aead": 64, "xor": 48, "wire": 92, "store": 76}[args.mode])
+        open_bytes = n * (2 * L + {"aead": 65, "xor": 48, "wire": 81, "store": 109}[args.mode])
         seal_gbs = seal_bytes / (seal_ms * 1e-3) / 1e9
         open_gbs = open_bytes / (open_ms * 1e-3) / 1e9
         dom = "seal" if seal_ms >= open_ms else "open"
@@ -410,7 +438,7 @@ def main():
             lanes = E.lanes_per_record(n, n * L, L)
             want = f"records_kernel<{lanes.bit_length() - 1}, {1 if dom == 'seal' else 2}, 0, 1>"
             k = next((v for name, v in pmc.get("kernels", {}).items() if want in name), None)
-            if k and pmc.get("config") == {"records": n, "record_bytes": L}:
+            if k and args.mode == "aead" and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
                 pmc_note = os.path.relpath(PMC_FILE, ROOT)
                 if "SQ_INSTS_VALU" in k:
@@ -428,7 +456,7 @@ def main():
                         "source": pmc_note,
                     }
         out = {
-            "metric": METRIC,
+            "metric": METRICS[args.mode],
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -441,8 +469,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic (torch.randint on device; random per-record keys and nonces)",
             "config": {
-                "workload": f"{WORKLOADS.get((n, L), 'custom')}: {n} x {L} B records, per-record (key, nonce), AEAD seal+open, "
-                            "device-resident",
+                "workload": f"{WORKLOADS.get((n, L), 'custom')}: {n} x {L} B records, per-record "
+                            f"(key, nonce), {MODE_DESC[args.mode]}, device-resident",
                 "records_per_gpu": n,
                 "record_bytes": L,
                 "lanes_per_record": E.lanes_per_record(n, n * L, L),
@@ -454,7 +482,8 @@ def main():
             "open_gibs": round(n * L / (open_ms * 1e-3) / 2**30, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"records_kernel ({dom})",
+                "kernel": (f"records_kernel ({dom})" if args.mode in ("aead", "xor")
+                           else f"{args.mode} {dom} kernel sequence"),
                 "achieved": round(dom_gbs, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

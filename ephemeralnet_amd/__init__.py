@@ -48,7 +48,9 @@ class _Records(C.Structure):
 EXPORTS = [
     "enet_chacha20_xor_batch", "enet_aead_seal_batch", "enet_aead_open_batch",
     "enet_sha256_batch", "enet_hmac_sha256_batch", "enet_hmac_sha256_verify_batch",
-    "enet_frame_seal_batch", "enet_frame_open_batch", "enet_aead_hmac_seal_batch",
+    "enet_frame_seal_batch", "enet_frame_open_batch", "enet_wire_seal_batch",
+    "enet_wire_open_batch", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
+    "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_last_error", "enet_abi_version",
 ]
@@ -74,6 +76,10 @@ def lib() -> C.CDLL:
         L.enet_hmac_sha256_verify_batch.argtypes = [u32, vp, vp, u32, vp, vp, vp, vp, vp]
         L.enet_frame_seal_batch.argtypes = [rp, vp]
         L.enet_frame_open_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_wire_seal_batch.argtypes = [rp, vp]
+        L.enet_wire_open_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_chunk_store_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_chunk_fetch_batch.argtypes = [rp, vp, vp, vp, vp]
         L.enet_aead_hmac_seal_batch.argtypes = [rp, vp, vp, vp]
         L.enet_aead_hmac_open_batch.argtypes = [rp, vp, vp, vp, vp]
         L.enet_chunk_counter.argtypes = [C.c_char_p]
@@ -207,6 +213,33 @@ def frame_open(b: Batch, out, out_offsets, macs, ok, stream=None) -> None:
     r = b.records(out, out_offsets)
     _check(lib().enet_frame_open_batch(C.byref(r), _ptr(macs), _ptr(ok), _stream(stream)),
            "enet_frame_open_batch")
+
+
+def wire_seal(b: Batch, out, out_offsets, stream=None) -> None:
+    """Whole wire frames nonce || BE32 len || ChaCha20(m || HMAC(m)) (SessionManager.cpp:362-387)."""
+    r = b.records(out, out_offsets)
+    _check(lib().enet_wire_seal_batch(C.byref(r), _stream(stream)), "enet_wire_seal_batch")
+
+
+def wire_open(b: Batch, out, out_offsets, macs, ok, stream=None) -> None:
+    """b.arena holds received wire frames; nonces come from the frames (b.nonces may be None)."""
+    r = b.records(out, out_offsets)
+    _check(lib().enet_wire_open_batch(C.byref(r), _ptr(macs), _ptr(ok), _stream(stream)),
+           "enet_wire_open_batch")
+
+
+def chunk_store(b: Batch, out, chunk_hashes, chunk_ids=None, stream=None) -> None:
+    """chunk_hashes = SHA-256(pt); out = ChaCha20 from LE32(chunk_id) (ids default to the hashes)."""
+    r = b.records(out, b.offsets)
+    _check(lib().enet_chunk_store_batch(C.byref(r), _ptr(chunk_ids), _ptr(chunk_hashes),
+                                        _stream(stream)), "enet_chunk_store_batch")
+
+
+def chunk_fetch(b: Batch, out, chunk_ids, chunk_hashes, ok, stream=None) -> None:
+    """out = decrypt; ok = SHA-256(out) == chunk_hashes (zeroed on mismatch)."""
+    r = b.records(out, b.offsets)
+    _check(lib().enet_chunk_fetch_batch(C.byref(r), _ptr(chunk_ids), _ptr(chunk_hashes), _ptr(ok),
+                                        _stream(stream)), "enet_chunk_fetch_batch")
 
 
 def chunk_counter(chunk_id: bytes) -> int:

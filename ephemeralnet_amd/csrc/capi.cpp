@@ -13,6 +13,9 @@
 
 #include "enet_internal.hpp"
 
+// nonce(12) || BE32 length (SessionManager.cpp:85-86,376-385)
+constexpr uint32_t kWireHeader = 16;
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -317,6 +320,109 @@ int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, voi
     s.zero_on_fail = r->out;
     s.order = r->order;
     return hip_status(enet::launch_sha(s, st), "frame_open hmac verify");
+}
+
+int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids, uint8_t* chunk_hashes,
+                           void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!chunk_hashes || !aligned4(chunk_hashes))
+        return fail(ENET_EINVAL, "chunk_store: chunk_hashes NULL or misaligned");
+    if (chunk_ids && !aligned4(chunk_ids)) return fail(ENET_EINVAL, "chunk_store: chunk_ids misaligned");
+    hipStream_t st = (hipStream_t)stream;
+    // 1) chunk_hash = SHA-256(pt) (Node.cpp:1414; = derive_chunk_id, StoreProof.cpp:75-78)
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->in;
+    s.off = r->in_offsets;
+    s.digest = chunk_hashes;
+    s.order = r->order;
+    if (int e = hip_status(enet::launch_sha(s, st), "chunk_store sha")) return e;
+    // 2) ChaCha20 from counter LE32(chunk_id[0..3]) (CryptoManager.cpp:8-13,38-46), the id read
+    //    on the device (the fresh digests when the caller derives ids from content)
+    enet::RecParams p = rec_params(r);
+    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids ? chunk_ids : chunk_hashes);
+    p.counter_stride = 8;
+    return hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
+                      "chunk_store chacha");
+}
+
+int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
+                           const uint8_t* chunk_hashes, uint8_t* ok, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!chunk_ids || !aligned4(chunk_ids) || !chunk_hashes || !ok)
+        return fail(ENET_EINVAL, "chunk_fetch: NULL/misaligned chunk_ids, NULL hashes or ok");
+    hipStream_t st = (hipStream_t)stream;
+    // 1) decrypt_with_key (CryptoManager.cpp:49-58)
+    enet::RecParams p = rec_params(r);
+    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids);
+    p.counter_stride = 8;
+    if (int e = hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
+                           "chunk_fetch chacha"))
+        return e;
+    // 2) SHA-256(pt) == manifest.chunk_hash, else no plaintext (Node.cpp:1644-1655)
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->out;
+    s.off = r->out_offsets;
+    s.expect = chunk_hashes;
+    s.ok = ok;
+    s.zero_on_fail = r->out;
+    s.order = r->order;
+    return hip_status(enet::launch_sha(s, st), "chunk_fetch sha verify");
+}
+
+int enet_wire_seal_batch(const enet_records* r, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    hipStream_t st = (hipStream_t)stream;
+    // 1) MAC = HMAC-SHA256(K, m) in clear at the tail of each frame body
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->in;
+    s.off = r->in_offsets;
+    s.digest = r->out + kWireHeader;
+    s.dest_off = r->out_offsets;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.order = r->order;
+    if (int e = hip_status(enet::launch_sha(s, st), "wire_seal hmac launch")) return e;
+    // 2) header + body = ChaCha20(ctr 0) over m || MAC
+    enet::RecParams p = rec_params(r);
+    p.hdr = kWireHeader;
+    return hip_status(enet::launch_records(3, p, lanes_for(r), st), "wire_seal chacha launch");
+}
+
+int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream) {
+    if (!r) return fail(ENET_EINVAL, "records descriptor is NULL");
+    if (r->count == 0) return ENET_OK;
+    enet_records q = *r;
+    static const uint32_t kNoNonce[3] = {0, 0, 0};
+    if (!q.nonces) q.nonces = reinterpret_cast<const uint8_t*>(kNoNonce);  // read from frames
+    if (int e = check_records(&q, true)) return e;
+    if (!macs || !ok) return fail(ENET_EINVAL, "wire_open: NULL macs/ok");
+    hipStream_t st = (hipStream_t)stream;
+    enet::RecParams p = rec_params(&q);
+    p.nonces = nullptr;
+    p.hdr = kWireHeader;
+    p.tag_out = macs;
+    if (int e = hip_status(enet::launch_records(4, p, lanes_for(r), st), "wire_open chacha"))
+        return e;
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->out;
+    s.off = r->out_offsets;
+    s.keys = r->keys;
+    s.key_stride = r->key_stride;
+    s.expect = macs;
+    s.ok = ok;
+    s.guard_off = r->in_offsets;
+    s.wire_in = r->in;
+    s.wire_hdr = kWireHeader;
+    s.zero_on_fail = r->out;
+    s.order = r->order;
+    return hip_status(enet::launch_sha(s, st), "wire_open hmac verify");
 }
 
 }  // extern "C"

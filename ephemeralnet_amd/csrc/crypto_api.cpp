@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <random>
 #include <stdexcept>
 #include <string>
 
@@ -446,6 +447,116 @@ std::vector<std::vector<std::uint8_t>> frame_open(std::span<const std::array<std
     enet_check(enet_frame_open_batch(&d.r, macs, dok, st.s()), "frame_open");
     st.d2h(ok.data(), dok, n);
     return download(st, d, out_off);
+}
+
+std::vector<StoredChunk> chunk_store(std::span<const Key> keys, std::span<const Nonce> nonces,
+                                     std::span<const std::span<const std::uint8_t>> chunks,
+                                     std::span<const ChunkId> chunk_ids) {
+    const size_t n = chunks.size();
+    if (keys.size() != n || nonces.size() != n || (!chunk_ids.empty() && chunk_ids.size() != n))
+        throw std::invalid_argument("enet batch::chunk_store: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(chunks);
+    auto kf = flat_keys(keys);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
+    auto* hashes = (uint8_t*)st.get(S_TAGS, 32 * n);
+    uint8_t* ids = nullptr;
+    if (!chunk_ids.empty()) {
+        ids = (uint8_t*)st.get(S_AUX, 32 * n);
+        st.h2d(ids, chunk_ids.data(), 32 * n);
+    }
+    enet_check(enet_chunk_store_batch(&d.r, ids, hashes, st.s()), "chunk_store");
+    std::vector<uint8_t> hh(32 * n);
+    st.d2h(hh.data(), hashes, 32 * n);
+    auto data = download(st, d, in.off);
+    std::vector<StoredChunk> res(n);
+    for (size_t i = 0; i < n; ++i) {
+        res[i].data = std::move(data[i]);
+        std::memcpy(res[i].chunk_hash.data(), hh.data() + 32 * i, 32);
+    }
+    return res;
+}
+
+std::vector<std::vector<std::uint8_t>> chunk_fetch(std::span<const Key> keys, std::span<const Nonce> nonces,
+                                                   std::span<const ChunkId> chunk_ids,
+                                                   std::span<const std::span<const std::uint8_t>> ciphertexts,
+                                                   std::span<const std::array<std::uint8_t, 32>> chunk_hashes,
+                                                   std::vector<std::uint8_t>& ok) {
+    const size_t n = ciphertexts.size();
+    if (keys.size() != n || nonces.size() != n || chunk_ids.size() != n || chunk_hashes.size() != n)
+        throw std::invalid_argument("enet batch::chunk_fetch: size mismatch");
+    ok.assign(n, 0);
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(ciphertexts);
+    auto kf = flat_keys(keys);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
+    auto* ids = (uint8_t*)st.get(S_AUX, 32 * n);
+    auto* hashes = (uint8_t*)st.get(S_TAGS, 32 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    st.h2d(ids, chunk_ids.data(), 32 * n);
+    st.h2d(hashes, chunk_hashes.data(), 32 * n);
+    enet_check(enet_chunk_fetch_batch(&d.r, ids, hashes, dok, st.s()), "chunk_fetch");
+    st.d2h(ok.data(), dok, n);
+    return download(st, d, in.off);
+}
+
+std::vector<std::vector<std::uint8_t>> wire_seal(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                                                 std::span<const Nonce> nonces,
+                                                 std::span<const std::span<const std::uint8_t>> messages) {
+    const size_t n = messages.size();
+    if (session_keys.size() != n || nonces.size() != n)
+        throw std::invalid_argument("enet batch::wire_seal: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(messages);
+    auto out_off = offsets_of(messages, 16 + 32);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
+    enet_check(enet_wire_seal_batch(&d.r, st.s()), "wire_seal");
+    return download(st, d, out_off);
+}
+
+std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                                                 std::span<const std::span<const std::uint8_t>> frames,
+                                                 std::vector<std::uint8_t>& ok) {
+    const size_t n = frames.size();
+    if (session_keys.size() != n) throw std::invalid_argument("enet batch::wire_open: size mismatch");
+    ok.assign(n, 0);
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(frames);
+    auto out_off = offsets_of(frames, -(16 + 32));
+    std::vector<uint8_t> no_nonces(12 * n, 0);  // unused: the nonce travels in the frame
+    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, no_nonces.data(), n);
+    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    enet_check(enet_wire_open_batch(&d.r, macs, dok, st.s()), "wire_open");
+    st.d2h(ok.data(), dok, n);
+    return download(st, d, out_off);
+}
+
+bool FrameQueue::push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message) {
+    if (message.size() + 32 > kMaxPayloadSize) return false;
+    Nonce nonce{};
+    std::random_device rd;
+    for (auto& byte : nonce.bytes) byte = static_cast<std::uint8_t>(rd());
+    keys_.push_back(session_key);
+    nonces_.push_back(nonce);
+    messages_.emplace_back(message.begin(), message.end());
+    return true;
+}
+
+std::vector<std::vector<std::uint8_t>> FrameQueue::flush() {
+    std::vector<std::span<const std::uint8_t>> views(messages_.begin(), messages_.end());
+    auto frames = wire_seal(keys_, nonces_, views);
+    keys_.clear();
+    nonces_.clear();
+    messages_.clear();
+    return frames;
 }
 
 }  // namespace batch

@@ -22,6 +22,7 @@ struct RecParams {
     uint32_t key_stride;
     const uint8_t* nonces;
     const uint32_t* counters;  // MODE_XOR start counters (nullable -> 0)
+    uint32_t counter_stride;   // words between records' counters (0 -> 1; 8 = LE32 of 32-B ids)
     const uint8_t* aad;        // nullable
     const uint64_t* aad_off;   // nullable
     const uint8_t* tag_in;     // open: expected tags
@@ -35,6 +36,10 @@ struct RecParams {
     uint64_t uniform_len;
     int coop;  // allow the cooperative-staging path for uniform batches
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
+    // wire frames (frame modes only): every frame starts with a hdr-byte header
+    // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the
+    // body; open reads the nonce from it.
+    uint32_t hdr;
 };
 
 // lanes: 1, 2, 4, 8 or 16 lanes per record.
@@ -55,6 +60,10 @@ struct ShaParams {
     const uint64_t* guard_off; // verify: records whose guard length is < 32 fail (Message.cpp:315)
     uint8_t* zero_on_fail;     // verify: arena (indexed like `in`) to zero for failed records
     int and_ok;                // verify: ok[i] &= (mac matches) instead of ok[i] = ...
+    // verify on wire frames: guard_off indexes the frames in wire_in; a frame shorter than
+    // wire_hdr + 32 or whose BE32 length field differs from its body length fails
+    const uint8_t* wire_in;
+    uint32_t wire_hdr;
     const uint32_t* order;     // nullable
 };
 hipError_t launch_sha(const ShaParams& p, hipStream_t s);

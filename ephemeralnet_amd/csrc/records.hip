@@ -102,6 +102,23 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         ooff = p.out_off[rec];
         Lout = p.out_off[rec + 1] - ooff;
     }
+    // wire frames: step over the nonce || BE32 length header
+    uint64_t frame0 = 0;                       // frame start (seal: header goes here)
+    bool hdr_ok = true;                        // open: the frame holds a whole header
+    if (FRAME != FR_NONE && p.hdr) {
+        if (FRAME == FR_SEAL) {
+            frame0 = ooff;
+            const uint64_t hb = min<uint64_t>(p.hdr, Lout);
+            ooff += hb;
+            Lout -= hb;
+        } else {
+            frame0 = ioff;
+            hdr_ok = Lin >= p.hdr;
+            const uint64_t hb = min<uint64_t>(p.hdr, Lin);
+            ioff += hb;
+            Lin -= hb;
+        }
+    }
     uint64_t L = Lin;                          // bytes run through the keystream
     if (FRAME == FR_SEAL) L = Lout;            // in || mac (mac sits in the out tail)
     uint64_t simple = L;                       // prefix where whole blocks take the fast path
@@ -121,9 +138,14 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         const uint32_t* kp = reinterpret_cast<const uint32_t*>(p.keys + (size_t)p.key_stride * rec);
 #pragma unroll
         for (int i = 0; i < 8; ++i) kw[i] = kp[i];
-        const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * rec);
+        if (FRAME == FR_OPEN && p.hdr) {  // nonce = first 12 bytes of the wire frame
 #pragma unroll
-        for (int i = 0; i < 3; ++i) nw[i] = np[i];
+            for (int i = 0; i < 3; ++i) nw[i] = hdr_ok ? ld32(p.in + frame0 + 4 * i) : 0u;
+        } else {
+            const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * rec);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nw[i] = np[i];
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) kw[i] = 0;
@@ -133,7 +155,8 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     ChachaRecord R;
     chacha_record_init(R, kw, nw);
     uint32_t ctr0 = 1;  // RFC 8439 data counter
-    if (MODE == MODE_XOR) ctr0 = (p.counters && live) ? p.counters[rec] : 0u;
+    if (MODE == MODE_XOR && p.counters && live)
+        ctr0 = p.counters[(size_t)rec * (p.counter_stride ? p.counter_stride : 1u)];
 
     // ---- Poly1305: one-time key from block 0; lane 0 absorbs the AAD prefix
     uint32_t h[5] = {0, 0, 0, 0, 0};
@@ -327,7 +350,7 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
                     const uint64_t q = pos + 4 * i + b;
                     const uint8_t byte = (uint8_t)(o[i] >> (8 * b));
                     if (q < Lout) dst[q] = byte;
-                    else if (q < L) p.tag_out[32ull * rec + (q - Lout)] = byte;
+                    else if (q < L && q - Lout < 32) p.tag_out[32ull * rec + (q - Lout)] = byte;
                 }
             }
         } else {
@@ -341,6 +364,20 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
                 if (4 * c + u < nct)
                     poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
         }
+    }
+
+    if (FRAME == FR_SEAL && p.hdr && live && j == 0 && Lout <= 0xFFFFFFFFull) {
+        // wire header: nonce(12) || BE32(|body|) (SessionManager.cpp:376-385)
+        uint8_t* hp = p.out + frame0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) hp[4 * i + b] = (uint8_t)(nw[i] >> (8 * b));
+        }
+        hp[12] = (uint8_t)(Lout >> 24);
+        hp[13] = (uint8_t)(Lout >> 16);
+        hp[14] = (uint8_t)(Lout >> 8);
+        hp[15] = (uint8_t)Lout;
     }
 
     if (kPoly) {

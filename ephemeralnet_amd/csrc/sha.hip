@@ -136,7 +136,17 @@ __global__ __launch_bounds__(kWG) void sha_kernel(ShaParams p) {
                                 ((uint32_t)e[4 * i + 2] << 8) | (uint32_t)e[4 * i + 3];
             diff |= ev ^ st[i];
         }
-        if (p.guard_off && (p.guard_off[rec + 1] - p.guard_off[rec]) < 32) diff = 1;
+        if (p.guard_off) {
+            const uint64_t g0 = p.guard_off[rec], glen = p.guard_off[rec + 1] - g0;
+            if (glen < 32ull + p.wire_hdr) {
+                diff = 1;
+            } else if (p.wire_in) {  // the receiver's length field must match the body it got
+                const uint8_t* lf = p.wire_in + g0 + 12;
+                const uint32_t be = ((uint32_t)lf[0] << 24) | ((uint32_t)lf[1] << 16) |
+                                    ((uint32_t)lf[2] << 8) | (uint32_t)lf[3];
+                if ((uint64_t)be != glen - p.wire_hdr) diff = 1;
+            }
+        }
         if (p.and_ok && p.ok[rec] == 0) diff |= 1;  // fused with an earlier check (AEAD tag)
         p.ok[rec] = diff == 0 ? 1 : 0;
         if (diff != 0 && p.zero_on_fail) {

@@ -109,6 +109,18 @@ ENET_API int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, cons
 ENET_API int enet_frame_seal_batch(const enet_records* r, void* stream);
 ENET_API int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
 
+/* ---- Whole wire frames (the batched session-frame codec): the frame body
+ *      above plus the 16-byte header, in one pass -- what SessionManager::send puts on the socket
+ *      (src/network/SessionManager.cpp:362-387) and what receive_loop takes off it (:760-822).
+ * seal: in_i = encoded message m_i, out_i = nonce_i(12) || BE32(|m_i|+32) || ChaCha20_{key_i,
+ *       nonce_i, 0}(m_i || HMAC_{key_i}(m_i)); out_offsets must give |out_i| = |m_i| + 48.
+ * open: in_i = a received frame; the nonce comes from the frame (r->nonces is ignored, may be
+ *       NULL); out_i = m_i (out_offsets must give |in_i| - 48), macs/ok as frame_open.  ok[i] = 0
+ *       also when the frame is shorter than 48 bytes or its length field differs from its body
+ *       length; failed messages are zeroed. */
+ENET_API int enet_wire_seal_batch(const enet_records* r, void* stream);
+ENET_API int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
+
 /* ---- AEAD with a fused HMAC-SHA256 integrity tag ("AEAD plus fused
  *      HMAC-SHA256 tag and verify").  The HMAC covers the plaintext under the record's 32-byte
  *      key, exactly what the reference signs before encrypting (encode_signed,
@@ -120,6 +132,20 @@ ENET_API int enet_aead_hmac_seal_batch(const enet_records* r, uint8_t* tags, uin
                                        void* stream);
 ENET_API int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags,
                                        const uint8_t* macs, uint8_t* ok, void* stream);
+
+/* ---- Chunk store / fetch pipeline (Node::store_chunk, src/core/Node.cpp:1414-1417,
+ *      Node::fetch_chunk's decrypt + hash check, :1641-1655).  in/out offsets equal-length.
+ * store: chunk_hashes[i] (device [n][32], 4-byte aligned) = SHA-256(in_i) -- the manifest
+ *        chunk_hash, and derive_chunk_id (src/security/StoreProof.cpp:75-78);
+ *        out_i = ChaCha20(key_i, nonce_i, LE32(chunk_id_i[0..3]), in_i) (encrypt_with_key,
+ *        CryptoManager.cpp:38-46) where chunk_id_i = chunk_ids[i], or the fresh chunk_hashes[i]
+ *        when chunk_ids == NULL (the daemon derives ids from content, ControlServer.cpp:1101).
+ * fetch: out_i = ChaCha20(key_i, nonce_i, LE32(chunk_ids[i][0..3]), in_i); ok[i] =
+ *        SHA-256(out_i) == chunk_hashes[i]; on mismatch out_i is zeroed (no plaintext). */
+ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids,
+                                    uint8_t* chunk_hashes, void* stream);
+ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
+                                    const uint8_t* chunk_hashes, uint8_t* ok, void* stream);
 
 /* ---- helpers (host) */
 /* LE32(chunk_id[0..3]) -- CryptoManager.cpp:8-13 derive_counter. */

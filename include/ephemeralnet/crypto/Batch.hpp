@@ -47,4 +47,51 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> frame_open(
     std::span<const std::array<std::uint8_t, 32>> session_keys, std::span<const Nonce> nonces,
     std::span<const std::span<const std::uint8_t>> bodies, std::vector<std::uint8_t>& ok);
 
+// Chunk store pipeline (Node.cpp:1414-1417): chunk_hash = SHA-256(chunk) and the chunk sealed by
+// CryptoManager::encrypt_with_key(key, chunk_id, chunk); chunk_ids empty = derive each id from
+// content (security::derive_chunk_id, as the daemon does, ControlServer.cpp:1101).
+struct StoredChunk {
+    std::vector<std::uint8_t> data;
+    std::array<std::uint8_t, 32> chunk_hash{};
+};
+ENET_CXX_API std::vector<StoredChunk> chunk_store(std::span<const Key> keys,
+                                                  std::span<const Nonce> nonces,
+                                                  std::span<const std::span<const std::uint8_t>> chunks,
+                                                  std::span<const ChunkId> chunk_ids);
+// Fetch side (Node.cpp:1641-1655): decrypt_with_key, then keep the plaintext only when its
+// SHA-256 equals the manifest's chunk_hash (ok[i] = 1); failed entries come back zeroed.
+ENET_CXX_API std::vector<std::vector<std::uint8_t>> chunk_fetch(
+    std::span<const Key> keys, std::span<const Nonce> nonces, std::span<const ChunkId> chunk_ids,
+    std::span<const std::span<const std::uint8_t>> ciphertexts,
+    std::span<const std::array<std::uint8_t, 32>> chunk_hashes, std::vector<std::uint8_t>& ok);
+
+// Whole wire frames nonce(12) || BE32(|body|) || ChaCha20_{K,N,0}(m || HMAC_K(m)) -- what
+// SessionManager::send writes (SessionManager.cpp:362-387) -- and their inverse, which takes the
+// nonce from the frame and rejects frames whose length field disagrees with the body.
+ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_seal(
+    std::span<const std::array<std::uint8_t, 32>> session_keys, std::span<const Nonce> nonces,
+    std::span<const std::span<const std::uint8_t>> messages);
+ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open(
+    std::span<const std::array<std::uint8_t, 32>> session_keys,
+    std::span<const std::span<const std::uint8_t>> frames, std::vector<std::uint8_t>& ok);
+
+// Send-side batching queue across sessions: callers push (session key,
+// encoded message) pairs from any session and one flush() seals them all in a single device
+// pass.  Nonces are drawn from std::random_device as in SessionManager::send (:366-372).
+class ENET_CXX_API FrameQueue {
+public:
+    static constexpr std::size_t kMaxPayloadSize = 1024 * 1024;  // SessionManager.cpp:87
+    // false when the signed payload (message + 32-byte MAC) exceeds kMaxPayloadSize, as
+    // SessionManager::send returns false (:358-360); nothing is queued then.
+    bool push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message);
+    std::size_t size() const { return messages_.size(); }
+    // wire frames in push order; empties the queue
+    std::vector<std::vector<std::uint8_t>> flush();
+
+private:
+    std::vector<std::array<std::uint8_t, 32>> keys_;
+    std::vector<Nonce> nonces_;
+    std::vector<std::vector<std::uint8_t>> messages_;
+};
+
 }  // namespace ephemeralnet::crypto::batch

@@ -12,6 +12,7 @@
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 #include "ephemeralnet/crypto/HmacSha256.hpp"
 #include "ephemeralnet/crypto/Sha256.hpp"
+#include "enet_crypto.h"
 
 using namespace ephemeralnet;
 
@@ -93,6 +94,49 @@ int main() {
             std::span<const uint8_t> bs[1] = {bodies[0]};
             auto back = crypto::batch::frame_open(std::span(&key, 1), std::span(&nonce, 1), bs, ok);
             std::cout << hex(bodies[0]) << " " << (ok[0] == 1 && back[0] == mb ? "1" : "0") << "\n";
+        } else if (op == "wire_queue") {
+            // SessionManager-style send queue across sessions, then the batched receive side
+            std::string k, m; in >> k >> m;
+            std::array<uint8_t, 32> key{};
+            auto kb = unhex(k);
+            std::copy(kb.begin(), kb.end(), key.begin());
+            auto mb = unhex(m);
+            crypto::batch::FrameQueue q;
+            const bool pushed = q.push(key, mb) && q.push(key, mb) && q.size() == 2;
+            std::vector<uint8_t> huge(crypto::batch::FrameQueue::kMaxPayloadSize - 31);
+            const bool refused = !q.push(key, huge) && q.size() == 2;
+            auto frames = q.flush();
+            std::vector<uint8_t> ok;
+            std::span<const uint8_t> fs[2] = {frames[0], frames[1]};
+            std::array<uint8_t, 32> ks[2] = {key, key};
+            auto back = crypto::batch::wire_open(ks, fs, ok);
+            const bool good = pushed && refused && q.size() == 0 && frames.size() == 2 &&
+                              ok[0] == 1 && ok[1] == 1 && back[0] == mb && back[1] == mb &&
+                              frames[0] != frames[1];
+            std::cout << hex(frames[0]) << " " << (good ? "1" : "0") << "\n";
+        } else if (op == "chunk_pipe") {
+            // Node::store_chunk / fetch_chunk crypto steps over the batch pipeline
+            std::string p; in >> p;
+            auto pb = unhex(p);
+            auto key = crypto::CryptoManager::generate_key();
+            crypto::Nonce nonce{};
+            nonce.bytes[0] = 7;
+            std::span<const uint8_t> ps[1] = {pb};
+            auto st = crypto::batch::chunk_store(std::span(&key, 1), std::span(&nonce, 1), ps, {});
+            ChunkId id{};
+            std::copy(st[0].chunk_hash.begin(), st[0].chunk_hash.end(), id.begin());
+            // the same ciphertext through the scalar reference API
+            auto ref = crypto::CryptoManager::encrypt_with_key(key, id, pb);
+            std::span<const uint8_t> cs[1] = {st[0].data};
+            std::vector<uint8_t> ok;
+            auto back = crypto::batch::chunk_fetch(std::span(&key, 1), std::span(&nonce, 1),
+                                                   std::span(&id, 1), cs, std::span(&st[0].chunk_hash, 1), ok);
+            std::vector<uint8_t> ct2;
+            crypto::ChaCha20::apply(key, nonce, pb, ct2, enet_chunk_counter(id.data()));
+            auto dec = crypto::CryptoManager::decrypt_with_key(key, id, st[0].data, nonce);
+            const bool good = ok[0] == 1 && back[0] == pb && ct2 == st[0].data &&
+                              ref.data.size() == pb.size() && dec && *dec == pb;
+            std::cout << hex(st[0].chunk_hash) << " " << (good ? "1" : "0") << "\n";
         } else if (op == "aead_seal") {
             std::string k, n, p; in >> k >> n >> p;
             crypto::Key key; crypto::Nonce nonce;

@@ -7,6 +7,8 @@ import subprocess
 
 import pytest
 
+import oracle
+
 from util import splitmix_bytes
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -70,6 +72,14 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         m = bytes.fromhex(f["signed"])[:-32]
         ops.append(f"frame_seal {f['key']} {f['nonce']} {h(m)}")
         expect.append(("eq", f"{f['body']} 1"))
+    for f in golden["frames"]:
+        m = bytes.fromhex(f["signed"])[:-32]
+        ops.append(f"wire_queue {f['key']} {h(m)}")
+        expect.append(("wire", (bytes.fromhex(f["key"]), m)))
+    for L in (0, 1, 64, 1500, 4096):
+        pt = splitmix_bytes(777 + L, L)
+        ops.append(f"chunk_pipe {h(pt)}")
+        expect.append(("eq", f"{hashlib.sha256(pt).hexdigest()} 1"))
     for c in golden["aead"]:
         if c["aad_len"] or c["len"] > 1500:
             continue
@@ -85,5 +95,12 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
                 assert got == (e["hex"] or "-"), op[:60]
             else:
                 assert hashlib.sha256(bytes.fromhex(got)).hexdigest() == e["sha256"]
+        elif kind == "wire":  # random nonce: check the frame against the oracle with its nonce
+            key, m = e
+            fr, flag = got.split()
+            fr = bytes.fromhex(fr)
+            nonce, body = fr[:12], fr[16:]
+            assert flag == "1" and int.from_bytes(fr[12:16], "big") == len(body) == len(m) + 32
+            assert body == oracle.frame_seal(key, nonce, m)
         else:
             assert got == e, op[:60]

@@ -130,6 +130,67 @@ def test_cryptomanager_golden(enet, golden):
         expect(c["ct"], g)
 
 
+# ------------------------------------------------------------------------------ chunk pipeline
+def test_chunk_store_golden(enet, golden):
+    """Store pipeline with caller-given chunk ids reproduces the reference's encrypt_with_key
+    ciphertexts, and the chunk hashes are SHA-256 of the plaintexts."""
+    import torch
+    cs = golden["cryptomanager"]
+    items = [splitmix_bytes(c["pt_seed"], c["len"]) for c in cs]
+    b = enet.make_batch(items, [bytes.fromhex(c["key"]) for c in cs], [bytes.fromhex(c["nonce"]) for c in cs])
+    ids = dev(b"".join(bytes.fromhex(c["chunk_id"]) for c in cs))
+    hashes = torch.zeros(32 * len(cs), dtype=torch.uint8, device="cuda")
+    out = out_like(b)
+    enet.chunk_store(b, out, hashes, chunk_ids=ids)
+    hh = host(hashes)
+    for i, (c, g) in enumerate(zip(cs, records_of(host(out), b.offsets.cpu().tolist()))):
+        expect(c["ct"], g)
+        assert hh[32 * i:32 * i + 32] == hashlib.sha256(items[i]).digest()
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_chunk_store_fetch_vs_oracle(enet, lanes):
+    """Content-derived ids (daemon store path): counter = LE32(SHA-256(chunk)[0..3]); the fetch
+    side decrypts and keeps only chunks whose hash matches the manifest."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 160
+    lens = rand_lengths(91, n, 9000)
+    lens[:6] = [0, 1, 63, 64, 4096, 65536]
+    items = [splitmix_bytes(3000 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(4000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(5000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces, base_offset=2)
+    hashes = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    ct = out_like(b)
+    enet.chunk_store(b, ct, hashes)
+    hh = host(hashes)
+    offs = b.offsets.cpu().tolist()
+    cts = records_of(host(ct), offs)
+    for i in range(n):
+        h = hashlib.sha256(items[i]).digest()
+        assert hh[32 * i:32 * i + 32] == h, i
+        ctr = int.from_bytes(h[:4], "little")
+        assert cts[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], ctr), i
+    # fetch: tamper one ciphertext byte and one manifest hash
+    ctb = bytearray(host(ct))
+    ctb[offs[10] + 3] ^= 0x01
+    bad_hashes = bytearray(hh)
+    bad_hashes[32 * 11] ^= 0x80
+    bf = enet.Batch(torch.frombuffer(ctb, dtype=torch.uint8).cuda(), b.offsets, b.keys, b.nonces,
+                    total_bytes_hint=b.total_bytes_hint, max_len_hint=b.max_len_hint)
+    back = torch.full_like(ct, 0x55)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.chunk_fetch(bf, back, hashes.clone(), dev(bytes(bad_hashes)), ok)
+    okh = ok.cpu().tolist()
+    got = records_of(host(back), offs)
+    for i in range(n):
+        if i in (10, 11):
+            assert okh[i] == 0 and got[i] == bytes(len(got[i])), i
+        else:
+            assert okh[i] == 1 and got[i] == items[i], i
+
+
 # ------------------------------------------------------------------------------ AEAD
 def aead_batch(enet, cases, base=0):
     import torch
@@ -340,6 +401,79 @@ def test_frames_random_vs_oracle(enet, lanes):
     bodies = records_of(host(out), ooffs.tolist())
     for i in range(n):
         assert bodies[i] == oracle.frame_seal(keys[i], nonces[i], msgs[i]), i
+
+
+# ------------------------------------------------------------------------------ wire frames
+def wire_of(nonce: bytes, body: bytes) -> bytes:
+    """SessionManager::send framing (SessionManager.cpp:376-387): nonce || BE32(len) || body."""
+    return nonce + len(body).to_bytes(4, "big") + body
+
+
+def wire_open_batch(enet, frames, keys):
+    import dataclasses
+
+    import torch
+    bo = dataclasses.replace(enet.make_batch(frames, keys, [b"\0" * 12] * len(frames),
+                                             base_offset=3), nonces=None)
+    poffs = np.concatenate([[0], np.cumsum([max(len(x) - 48, 0) for x in frames])]).astype(np.int64)
+    pt = torch.full((max(int(poffs[-1]), 1),), 0xAA, dtype=torch.uint8, device="cuda")
+    macs = torch.zeros(32 * len(frames), dtype=torch.uint8, device="cuda")
+    ok = torch.zeros(len(frames), dtype=torch.uint8, device="cuda")
+    enet.wire_open(bo, pt, torch.tensor(poffs).cuda(), macs, ok)
+    return records_of(host(pt), poffs.tolist()), ok.cpu().tolist()
+
+
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_wire_frames_golden(enet, golden, lanes):
+    """Whole wire frames against the reference's encode_signed bodies plus its framing; the
+    receive side rejects tampered bodies, wrong length fields, a tampered nonce and short frames."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    fs = golden["frames"]
+    msgs = [bytes.fromhex(f["signed"])[:-32] for f in fs]
+    keys = [bytes.fromhex(f["key"]) for f in fs]
+    nonces = [bytes.fromhex(f["nonce"]) for f in fs]
+    b = enet.make_batch(msgs, keys, nonces, base_offset=1)
+    ooffs = np.concatenate([[0], np.cumsum([len(m) + 48 for m in msgs])]).astype(np.int64)
+    out = torch.zeros(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
+    enet.wire_seal(b, out, torch.tensor(ooffs).cuda())
+    frames = records_of(host(out), ooffs.tolist())
+    for f, n, fr in zip(fs, nonces, frames):
+        assert fr == wire_of(n, bytes.fromhex(f["body"]))
+    good = len(frames)
+    bad = [
+        frames[0][:20] + bytes([frames[0][20] ^ 0x40]) + frames[0][21:],  # body bit flip
+        frames[0][:12] + (len(frames[0]) - 15).to_bytes(4, "big") + frames[0][16:],  # length
+        bytes([frames[0][0] ^ 1]) + frames[0][1:],  # nonce
+        frames[0][:47],  # shorter than header + MAC
+        frames[0][:10],  # shorter than the header
+    ]
+    got, okh = wire_open_batch(enet, frames + bad, keys + [keys[0]] * len(bad))
+    for i in range(good):
+        assert okh[i] == 1 and got[i] == msgs[i]
+    for i in range(good, good + len(bad)):
+        assert okh[i] == 0 and got[i] == bytes(len(got[i])), i
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 16])
+def test_wire_frames_random_vs_oracle(enet, lanes):
+    import torch
+    enet.set_lanes_per_record(lanes)
+    n = 300
+    lens = rand_lengths(78, n, 3000)
+    lens[:4] = [0, 1, 16, 1 << 14]
+    msgs = [splitmix_bytes(1900 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(51000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(61000 + i, 12) for i in range(n)]
+    b = enet.make_batch(msgs, keys, nonces, base_offset=5)
+    ooffs = np.concatenate([[7], 7 + np.cumsum([L + 48 for L in lens])]).astype(np.int64)
+    out = torch.zeros(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
+    enet.wire_seal(b, out, torch.tensor(ooffs).cuda())
+    frames = records_of(host(out), ooffs.tolist())
+    for i in range(n):
+        assert frames[i] == wire_of(nonces[i], oracle.frame_seal(keys[i], nonces[i], msgs[i])), i
+    got, okh = wire_open_batch(enet, frames, keys)
+    assert okh == [1] * n and got == msgs
 
 
 # ------------------------------------------------------------------------------ uniform (COOP)
