@@ -155,8 +155,10 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     ChachaRecord R;
     chacha_record_init(R, kw, nw);
     uint32_t ctr0 = 1;  // RFC 8439 data counter
-    if (MODE == MODE_XOR && p.counters && live)
-        ctr0 = p.counters[(size_t)rec * (p.counter_stride ? p.counter_stride : 1u)];
+    if (MODE == MODE_XOR)  // reference ChaCha20::apply counter (0 when not given)
+        ctr0 = (p.counters && live)
+                   ? p.counters[(size_t)rec * (p.counter_stride ? p.counter_stride : 1u)]
+                   : 0u;
 
     // ---- Poly1305: one-time key from block 0; lane 0 absorbs the AAD prefix
     uint32_t h[5] = {0, 0, 0, 0, 0};
