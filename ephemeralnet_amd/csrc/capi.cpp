@@ -300,7 +300,7 @@ int enet_frame_seal_batch(const enet_records* r, void* stream) {
 int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream) {
     if (int e = check_records(r, true)) return e;
     if (r->count == 0) return ENET_OK;
-    if (!macs || !ok) return fail(ENET_EINVAL, "frame_open: NULL macs/ok");
+    if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "frame_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
     // 1) decrypt: message bytes to out, MAC bytes to macs
     enet::RecParams p = rec_params(r);
@@ -401,7 +401,7 @@ int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void
     static const uint32_t kNoNonce[3] = {0, 0, 0};
     if (!q.nonces) q.nonces = reinterpret_cast<const uint8_t*>(kNoNonce);  // read from frames
     if (int e = check_records(&q, true)) return e;
-    if (!macs || !ok) return fail(ENET_EINVAL, "wire_open: NULL macs/ok");
+    if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "wire_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
     enet::RecParams p = rec_params(&q);
     p.nonces = nullptr;

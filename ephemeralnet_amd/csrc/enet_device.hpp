@@ -346,10 +346,37 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 }
 
 // ----------------------------------------------------------------------------- byte I/O
-// Load `n` (0..64) bytes at p into 16 LE words, zero beyond n.  Full blocks use four
-// 16-byte loads; the (at most one per record) partial block goes byte by byte.
+// Bytes [off, off + 4M) of the little-endian byte string in[0..4N) as M words, zero past the
+// end (off <= 4N).  The per-lane word offset goes through a log2(N)-stage barrel shift over
+// compile-time register indices (no dynamic VGPR indexing, no scratch), the byte offset through
+// v_alignbyte.  ~(N + 1) * log2(N) v_cndmask + M v_alignbyte.
+template <int N, int M>
+__device__ __forceinline__ void extract_bytes(const uint32_t* in, uint32_t off, uint32_t* out) {
+    constexpr int W = N + 1;
+    uint32_t a[W];
+#pragma unroll
+    for (int i = 0; i < N; ++i) a[i] = in[i];
+    a[N] = 0u;
+    const uint32_t k = off >> 2;
+#pragma unroll
+    for (int b = 32; b >= 1; b >>= 1) {
+        if (b > N) continue;
+        const bool t = (k & (uint32_t)b) != 0u;
+#pragma unroll
+        for (int i = 0; i < W; ++i) a[i] = t ? (i + b < W ? a[i + b] : 0u) : a[i];
+    }
+    const uint32_t sh = off & 3u;
+#pragma unroll
+    for (int j = 0; j < M; ++j)
+        out[j] = __builtin_amdgcn_alignbyte(j + 1 < W ? a[j + 1] : 0u, a[j], sh);
+}
+
+// Load `n` (1..64) bytes at p into 16 LE words, zero beyond n.  Full blocks: four 16-byte loads.
+// A partial block whose 16 bytes before p + n lie inside the record (window_ok) takes its whole
+// 16-byte chunks plus one 16-byte window ending at p + n, shifted into place in registers
+// (at most 4 loads); only records shorter than 16 bytes fall back to byte loads.
 __device__ __forceinline__ void load_block(const uint8_t* __restrict__ p, uint32_t n,
-                                           uint32_t w[16]) {
+                                           uint32_t w[16], bool window_ok = false) {
     if (n >= 64) {
         const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
@@ -357,8 +384,27 @@ __device__ __forceinline__ void load_block(const uint8_t* __restrict__ p, uint32
             const uint4 v = q[i];
             w[4 * i] = v.x; w[4 * i + 1] = v.y; w[4 * i + 2] = v.z; w[4 * i + 3] = v.w;
         }
+    } else if (window_ok) {
+        const uint32_t nq = n >> 4;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = 0u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if ((uint32_t)c < nq) {
+                const uint4 v = reinterpret_cast<const uint4*>(p)[c];
+                w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+            }
+        }
+        const uint4 v = *reinterpret_cast<const uint4*>(p + n - 16);
+        const uint32_t win[4] = {v.x, v.y, v.z, v.w};
+        uint32_t ch[4];
+        extract_bytes<4, 4>(win, 16u - (n & 15u), ch);  // the n mod 16 trailing bytes
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[4 * c + i] = ((uint32_t)c == nq) ? ch[i] : w[4 * c + i];
+        }
     } else {
-        // at most one partial block per record: predicated byte loads, compile-time indices
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             uint32_t v = 0;
@@ -370,6 +416,9 @@ __device__ __forceinline__ void load_block(const uint8_t* __restrict__ p, uint32
     }
 }
 
+// Store the first `n` (0..64) bytes of 16 LE words at p.  Partial blocks of >= 16 bytes: whole
+// 16-byte chunks plus one 16-byte window ending at p + n (rewriting bytes of the previous chunk
+// with the same values); shorter ones: whole words, then at most 3 bytes.
 __device__ __forceinline__ void store_block(uint8_t* __restrict__ p, uint32_t n,
                                             const uint32_t w[16]) {
     if (n >= 64) {
@@ -377,13 +426,25 @@ __device__ __forceinline__ void store_block(uint8_t* __restrict__ p, uint32_t n,
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             q[i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+    } else if (n >= 16) {
+        const uint32_t nq = n >> 4;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            if ((uint32_t)c < nq)
+                reinterpret_cast<uint4*>(p)[c] =
+                    make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+        uint32_t win[4];
+        extract_bytes<16, 4>(w, n - 16u, win);
+        *reinterpret_cast<uint4*>(p + n - 16) = make_uint4(win[0], win[1], win[2], win[3]);
     } else {
+        const uint32_t nw = n >> 2;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < 3; ++i)
+            if ((uint32_t)i < nw) *reinterpret_cast<uint32_t*>(p + 4 * i) = w[i];
+        const uint32_t lw = nw == 0 ? w[0] : nw == 1 ? w[1] : nw == 2 ? w[2] : w[3];
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if ((uint32_t)(4 * i + b) < n) p[4 * i + b] = (uint8_t)(w[i] >> (8 * b));
-        }
+        for (int b = 0; b < 3; ++b)
+            if ((uint32_t)b < (n & 3u)) p[4 * nw + b] = (uint8_t)(lw >> (8 * b));
     }
 }
 

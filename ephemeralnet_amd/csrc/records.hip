@@ -120,7 +120,8 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         }
     }
     uint64_t L = Lin;                          // bytes run through the keystream
-    if (FRAME == FR_SEAL) L = Lout;            // in || mac (mac sits in the out tail)
+    if (FRAME == FR_SEAL) L = Lout;            // in || mac (the HMAC pass left the MAC in
+                                               // clear at the tail of the out body)
     uint64_t simple = L;                       // prefix where whole blocks take the fast path
     if (FRAME == FR_SEAL) simple = Lin;
     if (FRAME == FR_OPEN) simple = Lout;
@@ -129,8 +130,8 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     const uint32_t cbeg = min(j * B, nb);
     const uint32_t cend = min(cbeg + B, nb);
     const uint32_t cfast = max(cbeg, min(cend, (uint32_t)(simple >> 6)));
-    const uint8_t* __restrict__ src = p.in + ioff;
-    uint8_t* __restrict__ dst = p.out + ooff;
+    const uint8_t* src = p.in + ioff;
+    uint8_t* dst = p.out + ooff;
 
     // ---- per-record ChaCha20 constants
     uint32_t kw[8], nw[3];
@@ -316,44 +317,63 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         for (int i = 0; i < 16; ++i) w[i] = wn[i];
     }
 
-    // ---- tail: the partial block and (frames) the blocks that touch the MAC
+    // ---- tail: the partial block and (frame open) the blocks that touch the MAC
+    uint32_t mac[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // frame open: MAC bytes this lane decrypted
     for (uint32_t c = cfast; c < cend; ++c) {
         const uint64_t pos = 64ull * c;
         const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
         if (FRAME == FR_SEAL && pos + 64 > Lin) {
-            // virtual input in[0, Lin) || out[Lin, Lout): the plaintext MAC written by the
-            // HMAC pass sits in the output record's tail
+            // virtual input m[pos, Lin) || MAC, the MAC (clear, at dst + Lin) shifted in place
+            const uint32_t nm = pos < Lin ? (uint32_t)(Lin - pos) : 0u;
+            if (nm) {
+                load_block(src + pos, nm, w, pos + nm >= 16);
+            } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint64_t q = pos + 4 * i + b;
-                    uint32_t byte = 0;
-                    if (q < Lin) byte = src[q];
-                    else if (q < L) byte = dst[q];
-                    v |= byte << (8 * b);
-                }
-                w[i] = v;
+                for (int i = 0; i < 16; ++i) w[i] = 0u;
             }
+            uint32_t m8[8];
+            {
+                const uint4 a = *reinterpret_cast<const uint4*>(dst + Lin);
+                const uint4 b = *reinterpret_cast<const uint4*>(dst + Lin + 16);
+                m8[0] = a.x; m8[1] = a.y; m8[2] = a.z; m8[3] = a.w;
+                m8[4] = b.x; m8[5] = b.y; m8[6] = b.z; m8[7] = b.w;
+            }
+            uint32_t ins[16];
+            if (pos <= Lin) {  // MAC bytes land at block offset Lin - pos
+                uint32_t z[24];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) z[i] = 0u;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) z[16 + i] = m8[i];
+                extract_bytes<24, 16>(z, 64u - (uint32_t)(Lin - pos), ins);
+            } else {           // the MAC's bytes [pos - Lin, 32) open this block
+                extract_bytes<8, 16>(m8, (uint32_t)(pos - Lin), ins);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] |= ins[i];
         } else {
-            load_block(src + pos, nbytes, w);
+            load_block(src + pos, nbytes, w, pos + nbytes >= 16);
         }
         uint32_t o[16];
         chacha_block(R, ctr0 + c, o);
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[i] ^= w[i];
-        if (FRAME == FR_OPEN && pos + 64 > Lout) {
-            // decrypted MAC (bytes >= Lout) goes to the tag buffer
+        if (FRAME == FR_OPEN) {
+            // message bytes [pos, Lout) to out; MAC bytes [Lout, Lout + 32) into mac[]
+            mask_tail(o, nbytes);
+            if (pos < Lout) store_block(dst + pos, (uint32_t)min<uint64_t>(64, Lout - pos), o);
+            if (pos + 64 > Lout && pos < Lout + 32) {
+                uint32_t part[8];
+                if (pos <= Lout) {
+                    extract_bytes<16, 8>(o, (uint32_t)(Lout - pos), part);
+                } else {  // MAC bytes [d, 32) from this block's bytes [0, 32 - d)
+                    uint32_t z[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint64_t q = pos + 4 * i + b;
-                    const uint8_t byte = (uint8_t)(o[i] >> (8 * b));
-                    if (q < Lout) dst[q] = byte;
-                    else if (q < L && q - Lout < 32) p.tag_out[32ull * rec + (q - Lout)] = byte;
+                    for (int i = 0; i < 8; ++i) { z[i] = 0u; z[8 + i] = o[i]; }
+                    extract_bytes<16, 8>(z, 32u - (uint32_t)(pos - Lout), part);
                 }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) mac[i] |= part[i];
             }
         } else {
             store_block(dst + pos, nbytes, o);
@@ -365,6 +385,19 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
             for (int u = 0; u < 4; ++u)
                 if (4 * c + u < nct)
                     poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
+        }
+    }
+    if (FRAME == FR_OPEN) {
+        // the MAC may straddle two lanes' segments: OR over the record's lanes, lane 0 writes
+#pragma unroll
+        for (uint32_t off = P >> 1; off >= 1; off >>= 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mac[i] |= __shfl_xor(mac[i], (int)off);
+        }
+        if (live && j == 0) {
+            uint32_t* mp = reinterpret_cast<uint32_t*>(p.tag_out + 32ull * rec);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mp[i] = mac[i];
         }
     }
 

@@ -34,19 +34,16 @@ __device__ __forceinline__ void sha_absorb_final(uint32_t st[8], const uint8_t* 
     // tail (0..63 bytes) + 0x80 + zeros + BE64 bit length, one or two blocks
     const uint32_t rem = (uint32_t)(len - done);
     const uint64_t bits = (prefix + len) * 8ull;
+    uint32_t wl[16];
+    if (rem) {
+        load_block(p + done, rem, wl, done + rem >= 16);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const uint32_t q = 4 * i + b;
-            uint32_t byte = 0;
-            if (q < rem) byte = p[done + q];
-            else if (q == rem) byte = 0x80;
-            v |= byte << (24 - 8 * b);
-        }
-        w[i] = v;
+        for (int i = 0; i < 16; ++i) wl[i] = 0u;
     }
+    const uint32_t mword = rem >> 2, mbit = 0x80u << (24 - 8 * (rem & 3u));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = bswap32(wl[i]) | ((uint32_t)i == mword ? mbit : 0u);
     if (rem >= 56) {
         sha256_compress(st, w);
 #pragma unroll
