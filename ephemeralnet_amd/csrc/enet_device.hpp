@@ -317,6 +317,11 @@ __constant__ static const uint32_t kSha256K[64] = {
 constexpr uint32_t kShaIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                                 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler emits two v_xor_b32
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // One compression (Sha256::transform, Sha256.cpp:134-176) on 16 big-endian message words.
 // The 64-entry schedule is kept as a rolling 16-word window in registers.
 __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
@@ -329,15 +334,15 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
             wi = w[i];
         } else {
             const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
             wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
             w[i & 15] = wi;
         }
-        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
         const uint32_t ch = (e & f) ^ (~e & g);
         const uint32_t t1 = h + S1 + ch + kSha256K[i] + wi;
-        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
         const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
