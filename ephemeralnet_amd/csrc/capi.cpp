@@ -72,6 +72,8 @@ enet::RecParams rec_params(const enet_records* r) {
         return s ? std::atoi(s) : 1;
     }();
     p.coop = coop_env;
+    // COOP 2 addresses the arena with 32-bit offsets
+    if (p.coop == 2 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
     return p;
 }
 

@@ -79,6 +79,12 @@ __device__ __forceinline__ void poly_block64(uint32_t h[5], const PolyR32& R, co
         asm volatile("" ::: "memory");        \
     } while (0)
 
+// Pin 16 register words: they must be computed before this point and cannot be sunk past it.
+#define ENET_PIN16(a)                                                                          \
+    asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), \
+                      "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), \
+                      "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])::"memory")
+
 constexpr uint32_t kStage = 2;                 // blocks per lane per cooperative stage
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
 
@@ -196,11 +202,11 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
             }
         }
     };
-    if (!COOP) poly_setup();
+    if (COOP == 0) poly_setup();
 
     // ---- cooperative stages (uniform batches)
     uint32_t cco = cbeg;  // first block left for the per-lane paths
-    if (COOP) {
+    if (COOP == 1) {
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t wbase = threadIdx.x & ~63u;
         const uint64_t Lu = p.uniform_len;
@@ -296,6 +302,93 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
             ENET_WAVE_LDS_SYNC();
             // (a) land the next stage in the slab
             land();
+        }
+        cco = min(cfast, cbeg + kStage * Ts);
+    }
+    if (COOP == 2) {
+        // Same whole-line stages and wave-private slab as COOP 1, but the loads go straight to
+        // LDS (global_load_lds_dwordx4: lane-linear destination, the chunk swizzle rides on the
+        // source address) and nothing is prefetched into registers.  The keystream does not
+        // depend on the data, so each stage's load flies under the same stage's ChaCha20
+        // rounds; the freed VGPRs buy more waves per SIMD to hide the LDS round trips.
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t wbase = threadIdx.x & ~63u;
+        const uint64_t Lu = p.uniform_len;
+        const uint32_t nfull = (uint32_t)(Lu >> 6);
+        const uint32_t jl = P - 1;
+        const uint32_t fmin = (nfull > jl * B) ? min(B, nfull - jl * B) : 0u;
+        const uint32_t Ts = fmin / kStage;
+        const uint32_t kk = lane & 7u;
+        const uint32_t wgid0 = blockIdx.x * kWG + wbase;
+        // 32-bit offsets from the arena bases (the host launches COOP 2 only when the batch
+        // spans < 4 GiB), so loads and stores take the SGPR-base + VGPR-offset form
+        uint32_t off[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t o = 8u * i + (lane >> 3);
+            const uint32_t og = (wgid0 + o) >> LOGP;
+            const uint32_t oj = (wgid0 + o) & (P - 1);
+            const uint32_t sw = (o >> 1) & 7u;
+            off[i] = (uint32_t)((uint64_t)og * Lu + 64ull * oj * B + 16u * (kk ^ sw));
+        }
+        const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
+        uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
+        uint8_t* wslab = slab + wbase * kRun;
+        uint8_t* myrun = slab + threadIdx.x * kRun;
+        const uint32_t msw = (lane >> 1) & 7u;
+        auto dma = [&](uint32_t stage) {
+            const uint32_t adv = kRun * stage;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                __builtin_amdgcn_global_load_lds(
+                    (__attribute__((address_space(1))) const void*)(ibase + (off[i] + adv)),
+                    (__attribute__((address_space(3))) void*)(wslab + 1024u * i), 16, 0, 0);
+        };
+        if (Ts > 0) dma(0);
+        poly_setup();
+        for (uint32_t st = 0; st < Ts; ++st) {
+            const uint32_t c0 = ctr0 + cbeg + kStage * st;
+            uint32_t ka[16], kb[16];
+            chacha_block2(R, c0, c0 + 1, ka, kb);
+            // keystream complete before the stage is read (else the scheduler hoists the LDS
+            // reads into the rounds and both sets of 32 words are live at once)
+            ENET_PIN16(ka);
+            ENET_PIN16(kb);
+            // the stage has landed (this also retires the previous stage's stores)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ENET_WAVE_LDS_SYNC();
+            uint32_t w2[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
+            }
+            if (MODE == MODE_OPEN) {
+                poly_block64(h, PR, w2);
+                poly_block64(h, PR, w2 + 16);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+            if (MODE == MODE_SEAL) {
+                poly_block64(h, PR, w2);
+                poly_block64(h, PR, w2 + 16);
+            }
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                    make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+            ENET_WAVE_LDS_SYNC();
+            const uint32_t adv = kRun * st;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                *reinterpret_cast<uint4*>(obase + (off[i] + adv)) = v;
+            }
+            // the stores above consumed every lane-linear read: the slab is free for the next
+            // stage's DMA
+            ENET_WAVE_LDS_SYNC();
+            if (st + 1 < Ts) dma(st + 1);
         }
         cco = min(cfast, cbeg + kStage * Ts);
     }
@@ -471,7 +564,7 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     const uint64_t lanes = (uint64_t)p.n << LOGP;
     const uint32_t blocks = (uint32_t)((lanes + kWG - 1) / kWG);
     if (blocks == 0) return hipSuccess;
-    if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop == 1) {
+    if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop >= 1) {
         // cooperative kernel over whole workgroups of records (no dead owners, no store
         // predicates); the remaining records go through the per-lane kernel
         const uint32_t per_wg = kWG >> LOGP;
@@ -479,8 +572,12 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG), 0,
-                               s, q);
+            if (p.coop == 2)
+                hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 2>), dim3(full), dim3(kWG),
+                                   0, s, q);
+            else
+                hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG),
+                                   0, s, q);
         }
         const uint32_t rest = p.n - full * per_wg;
         if (rest) {
