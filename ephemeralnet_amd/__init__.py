@@ -52,7 +52,8 @@ EXPORTS = [
     "enet_wire_open_batch", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
-    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_last_error", "enet_abi_version",
+    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_last_error",
+    "enet_abi_version",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -87,6 +88,7 @@ def lib() -> C.CDLL:
         L.enet_lanes_per_record.argtypes = [u32, u64, u32]
         L.enet_lanes_per_record.restype = u32
         L.enet_set_lanes_per_record.argtypes = [u32]
+        L.enet_set_staging.argtypes = [C.c_int]
         L.enet_last_error.restype = C.c_char_p
         L.enet_abi_version.restype = u32
         for name in EXPORTS:
@@ -254,6 +256,12 @@ def lanes_per_record(count: int, total_bytes: int = 0, max_len: int = 0) -> int:
 def set_lanes_per_record(lanes: int) -> None:
     """Force lanes per record (1/2/4/8/16); 0 restores the scheduler."""
     _check(lib().enet_set_lanes_per_record(lanes), "enet_set_lanes_per_record")
+
+
+def set_staging(variant: int) -> None:
+    """Uniform-batch staging variant: 1 register prefetch (default), 3 LDS DMA / four waves per
+    SIMD, 0 per-lane path only, -1 restores the default (results are identical)."""
+    _check(lib().enet_set_staging(variant), "enet_set_staging")
 
 
 def make_batch(items: Sequence[bytes], keys: Sequence[bytes], nonces: Sequence[bytes],

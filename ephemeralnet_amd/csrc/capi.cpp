@@ -67,13 +67,9 @@ enet::RecParams rec_params(const enet_records* r) {
     // offsets[0] + i * max, since records are contiguous by construction)
     if (r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint)
         p.uniform_len = r->max_len_hint;
-    static const int coop_env = [] {
-        const char* s = std::getenv("ENET_COOP");
-        return s ? std::atoi(s) : 1;
-    }();
-    p.coop = coop_env;
-    // COOP 2 addresses the arena with 32-bit offsets
-    if (p.coop == 2 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
+    p.coop = (int)enet::staging_variant();
+    // COOP 3 addresses the arena with 32-bit offsets
+    if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
     return p;
 }
 
@@ -86,6 +82,20 @@ uint32_t lanes_for(const enet_records* r) {
 namespace enet {
 
 static std::atomic<uint32_t> g_forced_lanes{0};
+static std::atomic<uint32_t> g_staging{0};
+
+// Uniform-batch staging: 1 = register prefetch + LDS transposition (default), 3 = LDS DMA,
+// one live keystream block, four waves per SIMD; 0 = per-lane path only.  ENET_COOP /
+// enet_set_staging override (tuning / tests).
+uint32_t staging_variant() {
+    static const uint32_t env = [] {
+        const char* s = std::getenv("ENET_COOP");
+        return s ? (uint32_t)std::strtoul(s, nullptr, 10) + 1u : 0u;
+    }();
+    if (uint32_t f = g_staging.load(std::memory_order_relaxed)) return f - 1u;
+    if (env == 1 || env == 2 || env == 4) return env - 1u;
+    return 1u;
+}
 
 // Give each record enough lanes that the grid holds >= ENET_TARGET_LANES lanes
 // (default 2 waves per SIMD on 256 CUs = 131072), but keep >= 8 ChaCha20 blocks per lane: every
@@ -128,6 +138,13 @@ uint32_t enet_chunk_counter(const uint8_t chunk_id[32]) {  // CryptoManager.cpp:
 
 uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t max_len) {
     return enet::choose_lanes(count, total_bytes, max_len);
+}
+
+int enet_set_staging(int variant) {
+    if (variant != -1 && variant != 0 && variant != 1 && variant != 3)
+        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1 or 3");
+    enet::g_staging.store((uint32_t)(variant + 1), std::memory_order_relaxed);
+    return ENET_OK;
 }
 
 int enet_set_lanes_per_record(uint32_t lanes) {

@@ -34,7 +34,7 @@ struct RecParams {
     const uint8_t* append;
     // uniform batch: every record is exactly uniform_len bytes in and out (0 = not uniform)
     uint64_t uniform_len;
-    int coop;  // allow the cooperative-staging path for uniform batches
+    int coop;  // uniform-batch staging variant: 0 none, 1 register prefetch, 3 LDS DMA
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the
@@ -70,5 +70,6 @@ hipError_t launch_sha(const ShaParams& p, hipStream_t s);
 
 
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
+uint32_t staging_variant();
 
 }  // namespace enet

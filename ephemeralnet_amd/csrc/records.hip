@@ -89,7 +89,7 @@ constexpr uint32_t kStage = 2;                 // blocks per lane per cooperativ
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
 
 template <int LOGP, int MODE, int FRAME, int COOP>
-__global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
+__device__ __forceinline__ void records_body(const RecParams& p) {
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
     __shared__ __attribute__((aligned(16))) uint8_t slab[COOP ? kWG * kRun : 16];
@@ -305,12 +305,15 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         }
         cco = min(cfast, cbeg + kStage * Ts);
     }
-    if (COOP == 2) {
+    if (COOP == 3) {
         // Same whole-line stages and wave-private slab as COOP 1, but the loads go straight to
         // LDS (global_load_lds_dwordx4: lane-linear destination, the chunk swizzle rides on the
-        // source address) and nothing is prefetched into registers.  The keystream does not
-        // depend on the data, so each stage's load flies under the same stage's ChaCha20
-        // rounds; the freed VGPRs buy more waves per SIMD to hide the LDS round trips.
+        // source address), nothing is prefetched into registers and only ONE keystream block
+        // is live at a time: the kernel fits in <= 128 VGPRs (four waves per SIMD).  The
+        // keystream does not depend on the data, so each stage's DMA flies under the rounds of
+        // its first block; block 1's own-run reads are issued before its keystream is computed.
+        // 32-bit offsets from the arena bases (the host launches it only for batches < 4 GiB),
+        // so loads and stores take the SGPR-base + VGPR-offset form.
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t wbase = threadIdx.x & ~63u;
         const uint64_t Lu = p.uniform_len;
@@ -320,8 +323,6 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
         const uint32_t Ts = fmin / kStage;
         const uint32_t kk = lane & 7u;
         const uint32_t wgid0 = blockIdx.x * kWG + wbase;
-        // 32-bit offsets from the arena bases (the host launches COOP 2 only when the batch
-        // spans < 4 GiB), so loads and stores take the SGPR-base + VGPR-offset form
         uint32_t off[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -344,46 +345,55 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
                     (__attribute__((address_space(1))) const void*)(ibase + (off[i] + adv)),
                     (__attribute__((address_space(3))) void*)(wslab + 1024u * i), 16, 0, 0);
         };
+        auto read_own = [&](int b, uint32_t d[16]) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * ((4u * b + k) ^ msw));
+                d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+            }
+        };
+        auto finish_block = [&](int b, uint32_t d[16], const uint32_t ks[16]) {
+            if (MODE == MODE_OPEN) poly_block64(h, PR, d);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) d[i] ^= ks[i];
+            if (MODE == MODE_SEAL) poly_block64(h, PR, d);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                *reinterpret_cast<uint4*>(myrun + 16u * ((4u * b + k) ^ msw)) =
+                    make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+        };
         if (Ts > 0) dma(0);
         poly_setup();
         for (uint32_t st = 0; st < Ts; ++st) {
             const uint32_t c0 = ctr0 + cbeg + kStage * st;
-            uint32_t ka[16], kb[16];
-            chacha_block2(R, c0, c0 + 1, ka, kb);
-            // keystream complete before the stage is read (else the scheduler hoists the LDS
-            // reads into the rounds and both sets of 32 words are live at once)
-            ENET_PIN16(ka);
-            ENET_PIN16(kb);
+            uint32_t d[16], ks[16];
+            chacha_block(R, c0, ks);
+            ENET_PIN16(ks);
             // the stage has landed (this also retires the previous stage's stores)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ENET_WAVE_LDS_SYNC();
-            uint32_t w2[32];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
-                w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
-            }
-            if (MODE == MODE_OPEN) {
-                poly_block64(h, PR, w2);
-                poly_block64(h, PR, w2 + 16);
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
-            if (MODE == MODE_SEAL) {
-                poly_block64(h, PR, w2);
-                poly_block64(h, PR, w2 + 16);
-            }
+            read_own(0, d);
+            finish_block(0, d, ks);
+            read_own(1, d);
             ENET_WAVE_LDS_SYNC();
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
-                    make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+            chacha_block(R, c0 + 1, ks);
+            ENET_PIN16(ks);
+            finish_block(1, d, ks);
             ENET_WAVE_LDS_SYNC();
             const uint32_t adv = kRun * st;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
-                *reinterpret_cast<uint4*>(obase + (off[i] + adv)) = v;
+            for (int hh = 0; hh < 2; ++hh) {
+                uint32_t v[16];  // plain words: a uint4 array would be kept in scratch
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 t =
+                        *reinterpret_cast<const uint4*>(wslab + 1024u * (4 * hh + i) + 16u * lane);
+                    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    *reinterpret_cast<uint4*>(obase + (off[4 * hh + i] + adv)) =
+                        make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
             }
             // the stores above consumed every lane-linear read: the slab is free for the next
             // stage's DMA
@@ -559,6 +569,18 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     }
 }
 
+template <int LOGP, int MODE, int FRAME, int COOP>
+__global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
+    records_body<LOGP, MODE, FRAME, COOP>(p);
+}
+
+// COOP 3 is built to fit four waves per SIMD (<= 128 VGPRs)
+template <int LOGP, int MODE>
+__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(4)))
+void records_kernel_w4(RecParams p) {
+    records_body<LOGP, MODE, FR_NONE, 3>(p);
+}
+
 template <int LOGP, int MODE, int FRAME>
 static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     const uint64_t lanes = (uint64_t)p.n << LOGP;
@@ -572,9 +594,8 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            if (p.coop == 2)
-                hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 2>), dim3(full), dim3(kWG),
-                                   0, s, q);
+            if (p.coop == 3)
+                hipLaunchKernelGGL((records_kernel_w4<LOGP, MODE>), dim3(full), dim3(kWG), 0, s, q);
             else
                 hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG),
                                    0, s, q);

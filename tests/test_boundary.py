@@ -82,6 +82,10 @@ def test_library_loads_and_host_helpers(built):
     with pytest.raises(E.EnetError):
         E.set_lanes_per_record(3)
     E.set_lanes_per_record(0)
+    with pytest.raises(E.EnetError):
+        E.set_staging(2)
+    E.set_staging(3)
+    E.set_staging(-1)
 
 
 def test_invalid_arguments_rejected_without_gpu(built):

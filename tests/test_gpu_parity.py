@@ -477,15 +477,17 @@ def test_wire_frames_random_vs_oracle(enet, lanes):
 
 
 # ------------------------------------------------------------------------------ uniform (COOP)
+@pytest.mark.parametrize("staging", [1, 3, 0])
 @pytest.mark.parametrize("L,n,lanes", [(1500, 1000, 1), (1500, 517, 2), (4096, 300, 2),
                                        (4096, 129, 4), (65536, 40, 8), (65536, 33, 16),
                                        (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1)])
-def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes):
-    """Uniform-length batches take the cooperative LDS-staged path (whole workgroups) plus the
-    per-lane path for the partial workgroup; 1500-byte records start unaligned and end in a
-    partial block."""
+def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes, staging):
+    """Uniform-length batches take the cooperative LDS-staged path (whole workgroups; staging
+    variant 1 = register prefetch, 3 = LDS DMA) plus the per-lane path for the partial
+    workgroup; 1500-byte records start unaligned and end in a partial block."""
     import torch
     enet.set_lanes_per_record(lanes)
+    enet.set_staging(staging)
     items = [splitmix_bytes(70000 + i, L) for i in range(n)]
     keys = [splitmix_bytes(80000 + i, 32) for i in range(n)]
     nonces = [splitmix_bytes(90000 + i, 12) for i in range(n)]
@@ -514,6 +516,7 @@ def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes):
     xg = records_of(host(xo), b.offsets.cpu().tolist())
     for i in list(idx)[:64]:
         assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i]))
+    enet.set_staging(-1)
 
 
 # ------------------------------------------------------------------------------ AEAD + HMAC (C5)

@@ -1,0 +1,199 @@
+// ubench_mix2.hip -- which VALU instruction forms reach the 2-cycle (two waves interleaved)
+// issue rate on gfx950 and which stay at 4?  Event-timed, 8 independent chains per lane,
+// 1/2/4 waves per SIMD.  Prints cycles per wave64 instruction per SIMD at the measured clock
+// assumption of 2.4 GHz.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
+
+template <int V>
+__global__ __launch_bounds__(256) void k_mix(uint32_t* out, int iters, uint32_t seed) {
+    uint32_t x[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = seed * (i + 1) + threadIdx.x * 77u + blockIdx.x;
+    uint64_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = x[i] * 0x9e3779b97f4a7c15ull;
+    uint32_t b = seed ^ 0x9e3779b9u, c = seed * 3u + 1u;
+    asm volatile("" : "+v"(b), "+v"(c));
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t& a = x[i];
+                uint32_t& o = x[(i + 4) & 7];
+                if (V == 0) asm volatile("v_or_b32_e32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 1) asm volatile("v_sub_u32_e32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 2) asm volatile("v_ashrrev_i32_e32 %0, 7, %0" : "+v"(a));
+                if (V == 3) asm volatile("v_not_b32_e32 %0, %0" : "+v"(a));
+                if (V == 4) asm volatile("v_bfe_u32 %0, %0, 3, 9" : "+v"(a));
+                if (V == 5) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+                if (V == 6) asm volatile("v_alignbyte_b32 %0, %0, %0, 1" : "+v"(a));
+                if (V == 7) asm volatile("v_lshlrev_b32_e32 %0, %1, %0" : "+v"(a) : "v"(b));
+                if (V == 8) asm volatile("v_lshlrev_b32_e64 %0, 7, %0" : "+v"(a));
+                if (V == 9) asm volatile("v_lshlrev_b16_e32 %0, 7, %0" : "+v"(a));
+                if (V == 10) asm volatile("v_pk_lshlrev_b16 %0, 7, %0" : "+v"(a));
+                if (V == 11) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 12) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 13) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0" : "+v"(a) : "v"(o));
+                if (V == 14) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1" : "+v"(a) : "v"(b));
+                if (V == 15) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0" : "+v"(a) : "v"(b));
+                if (V == 16) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "+v"(a) : "v"(b));
+                if (V == 17) asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "+v"(a) : "v"(b));
+                if (V == 18) asm volatile("v_lshlrev_b32_sdwa %0, 7, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD" : "+v"(a));
+                if (V == 19) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(w[i]) : "v"(a), "v"(b) : "vcc");
+                if (V == 20) asm volatile("v_lshrrev_b64 %0, 7, %0" : "+v"(w[i]));
+                if (V == 21) asm volatile("v_lshlrev_b64 %0, 7, %0" : "+v"(w[i]));
+                if (V == 22) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(w[i]) : "v"(w[(i + 3) & 7]));
+                if (V == 23) asm volatile("v_pk_mov_b32 %0, %0, %1 op_sel:[1,0]" : "+v"(w[i]) : "v"(w[(i + 3) & 7]));
+                if (V == 24) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+                if (V == 25) asm volatile("v_subrev_u32_e32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 26) asm volatile("v_max_u32_e32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 27) asm volatile("v_cvt_f32_u32_e32 %0, %0" : "+v"(a));
+                if (V == 28) asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(a) : "v"(b));
+                if (V == 29) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+                if (V == 30) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(w[i]) : "v"(w[(i + 3) & 7]));
+                if (V == 31) asm volatile("v_pk_fma_f32 %0, %0, %1, %0" : "+v"(w[i]) : "v"(w[(i + 3) & 7]));
+            }
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= x[i] ^ (uint32_t)w[i] ^ (uint32_t)(w[i] >> 32);
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+// ChaCha quarter-round chains written as explicit asm, 8 columns (2 blocks), varied forms.
+#define QRA(a, b, c, d, R16, R12, R8, R7)                                       \
+    asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a) : "v"(b));                \
+    asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(d) : "v"(a));                \
+    R16(d);                                                                     \
+    asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(c) : "v"(d));                \
+    asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(b) : "v"(c));                \
+    R12(b);                                                                     \
+    asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(a) : "v"(b));                \
+    asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(d) : "v"(a));                \
+    R8(d);                                                                      \
+    asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(c) : "v"(d));                \
+    asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(b) : "v"(c));                \
+    R7(b);
+#define ROT_AB(n) [&](uint32_t& v) { asm volatile("v_alignbit_b32 %0, %0, %0, " #n : "+v"(v)); }
+
+template <int V>
+__global__ __launch_bounds__(256) void k_qr(uint32_t* out, int iters, uint32_t seed) {
+    uint32_t x[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) x[i] = seed * (i + 1) + threadIdx.x * 77u + blockIdx.x;
+    auto r16 = ROT_AB(16);
+    auto r12 = ROT_AB(20);
+    auto r8 = ROT_AB(24);
+    auto r7 = ROT_AB(25);
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            if (V == 0) {  // column + diagonal rounds, QR by QR (compiler may not reorder asm volatile)
+#pragma unroll
+                for (int blk = 0; blk < 2; ++blk) {
+                    uint32_t* y = x + 16 * blk;
+                    QRA(y[0], y[4], y[8], y[12], r16, r12, r8, r7);
+                    QRA(y[1], y[5], y[9], y[13], r16, r12, r8, r7);
+                    QRA(y[2], y[6], y[10], y[14], r16, r12, r8, r7);
+                    QRA(y[3], y[7], y[11], y[15], r16, r12, r8, r7);
+                }
+            } else {  // 8 QRs interleaved step by step (what the compiler emits)
+#define STEP(OP) for (int q = 0; q < 8; ++q) { uint32_t* y = x + 16 * (q >> 2); const int k = q & 3; OP; }
+                STEP(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(y[k]) : "v"(y[4 + k])));
+                STEP(asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(y[12 + k]) : "v"(y[k])));
+                STEP(r16(y[12 + k]));
+                STEP(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(y[8 + k]) : "v"(y[12 + k])));
+                STEP(asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(y[4 + k]) : "v"(y[8 + k])));
+                STEP(r12(y[4 + k]));
+                STEP(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(y[k]) : "v"(y[4 + k])));
+                STEP(asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(y[12 + k]) : "v"(y[k])));
+                STEP(r8(y[12 + k]));
+                STEP(asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(y[8 + k]) : "v"(y[12 + k])));
+                STEP(asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(y[4 + k]) : "v"(y[8 + k])));
+                STEP(r7(y[4 + k]));
+#undef STEP
+            }
+        }
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc ^= x[i];
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+template <typename F>
+static double run(F launch, int occ, double instr_per_iter, int iters, hipEvent_t e0, hipEvent_t e1) {
+    launch(occ, 20);
+    hipEventRecord(e0);
+    launch(occ, iters);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    return ms * 1e-3 * 2.4e9 / (occ * (double)iters * instr_per_iter);
+}
+
+#define MIX(V, NAME)                                                                            \
+    for (int occ : {1, 2, 4}) {                                                                 \
+        double c = run([&](int o, int it) { hipLaunchKernelGGL(k_mix<V>, dim3(256 * o), dim3(256), 0, 0, d, it, 1u); }, \
+                       occ, 128.0, 2000, e0, e1);                                               \
+        printf("{\"form\":\"%s\",\"waves_per_simd\":%d,\"cyc\":%.3f}\n", NAME, occ, c);       \
+    }
+
+int main() {
+    uint32_t* d;
+    CK(hipMalloc(&d, 64 << 20));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_mix<0>, dim3(4096), dim3(256), 0, 0, d, 20000, 1u);
+    CK(hipDeviceSynchronize());
+    MIX(0, "v_or_b32 a,a,b");
+    MIX(1, "v_sub_u32 a,a,b");
+    MIX(2, "v_ashrrev_i32 a,7,a");
+    MIX(3, "v_not_b32 a,a");
+    MIX(4, "v_bfe_u32 a,a,3,9");
+    MIX(5, "v_bfi_b32 a,a,b,c");
+    MIX(6, "v_alignbyte a,a,a,1");
+    MIX(7, "v_lshlrev_b32 a,vb,a");
+    MIX(8, "v_lshlrev_b32_e64 a,7,a");
+    MIX(9, "v_lshlrev_b16 a,7,a");
+    MIX(10, "v_pk_lshlrev_b16 a,7,a");
+    MIX(11, "v_mul_lo_u32 a,a,b");
+    MIX(12, "v_mul_hi_u32 a,a,b");
+    MIX(13, "v_mov_b32_sdwa a.hi=o.lo");
+    MIX(14, "v_xor_b32_sdwa lo=a.hi^b.hi");
+    MIX(15, "v_xor_b32_sdwa hi=a.lo^b.lo preserve");
+    MIX(16, "v_add_u32_sdwa byte1");
+    MIX(17, "v_or_b32_sdwa src1 word1");
+    MIX(18, "v_lshlrev_b32_sdwa a,7,a");
+    MIX(19, "v_mad_u64_u32");
+    MIX(20, "v_lshrrev_b64");
+    MIX(21, "v_lshlrev_b64");
+    MIX(22, "v_lshl_add_u64 (add64)");
+    MIX(23, "v_pk_mov_b32");
+    MIX(24, "v_or3_b32");
+    MIX(25, "v_subrev_u32 a,a,b");
+    MIX(26, "v_max_u32");
+    MIX(27, "v_cvt_f32_u32");
+    MIX(28, "v_add_f32");
+    MIX(29, "v_fma_f32");
+    MIX(30, "v_pk_add_f32");
+    MIX(31, "v_pk_fma_f32");
+    for (int v = 0; v < 2; ++v)
+        for (int occ : {1, 2, 4}) {
+            double c = run([&](int o, int it) {
+                if (v == 0) hipLaunchKernelGGL(k_qr<0>, dim3(256 * o), dim3(256), 0, 0, d, it, 1u);
+                else hipLaunchKernelGGL(k_qr<1>, dim3(256 * o), dim3(256), 0, 0, d, it, 1u);
+            }, occ, 10 * 8 * 12.0, 500, e0, e1);
+            printf("{\"form\":\"chacha_qr_%s\",\"waves_per_simd\":%d,\"cyc\":%.3f}\n",
+                   v == 0 ? "sequential" : "interleaved8", occ, c);
+        }
+    return 0;
+}
