@@ -25,9 +25,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
-# int32 VALU: one wave64 instruction per 4 cycles per SIMD (measured: SQ_ACTIVE_INST_VALU equals
-# SQ_INSTS_VALU in quad-cycles, tools/ubench.hip) -> 256 CU x 4 SIMD x 16 lanes x 2.4 GHz
-VALU_PEAK_TOPS = 39.3
+# VALU: gfx950 issues a full-rate wave64 op (v_add/v_xor/v_lshrrev/v_bitop3 ...) every 2 cycles per
+# SIMD once two waves share it, half-rate ops (v_alignbit = the ChaCha rotate, v_mad_u64_u32 =
+# the Poly1305 limb product, carries) every 4+ (tools/ubench_mix*.hip).  The binding ceiling of
+# this kernel is therefore its own instruction mix: the compute-only rate of the same stage body
+# with no memory traffic (tools/ubench_seal.hip), committed in VALU_CEILING_FILE.
+VALU_ISSUE_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, full-rate ops only
 WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
 MODE_DESC = {"aead": "AEAD seal+open", "xor": "ChaCha20 xor twice",
@@ -40,6 +43,7 @@ METRICS = {  # the headline is `aead`; the others are SURVEY 8d/8f side measurem
     "store": "GiB/s chunk store+fetch pipeline, SHA-256 + ChaCha20 (device-resident)",
 }
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r01.json")
+VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "valu_ceiling_r01.json")
 
 
 def parse():
@@ -55,9 +59,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate wall budget of the CPU baseline sample")
     ap.add_argument("--e2e", action="store_true",
-                    help="host-resident path: pinned host buffers, H2D -> kernel -> D2H pipelined "
-                         "over 3 streams in 16 MiB chunks (recorded in DESIGN.md, never `value`)")
-    ap.add_argument("--chunk-records", type=int, default=4096)
+                    help="host-resident path through the library's host pipeline: pinned host "
+                         "buffers, H2D -> kernel -> D2H overlapped over --streams streams in "
+                         "--chunk-mib chunks (recorded in DESIGN.md, never `value`)")
+    ap.add_argument("--chunk-mib", type=int, default=16, help="host pipeline chunk size")
+    ap.add_argument("--streams", type=int, default=3, help="host pipeline streams")
+    ap.add_argument("--c5-chunk-mib", type=int, default=64,
+                    help="host pipeline chunk size for --c5 (one lane hashes a whole record, so "
+                         "mixed batches with HMAC want big chunks)")
     ap.add_argument("--c5", action="store_true",
                     help="SURVEY 8d C5: log-uniform 512 B-64 KiB records, AEAD + fused HMAC-SHA256, "
                          "host-resident (H2D + kernels + D2H), records per GPU = --records")
@@ -125,81 +134,58 @@ def cpu_baseline(record_bytes: int, budget_s: float) -> dict:
 
 
 def e2e(args) -> dict:
-    """Seal and open with the data starting and ending in (pinned) host memory, as the
-    reference's socket/relay path does: chunk k goes H2D on stream k%3, is sealed/opened there and
-    comes back D2H, so copies of one chunk overlap the kernels of the others.  Session keys stay
-    resident on the device; nonces travel with the data."""
+    """Seal and open with the data starting and ending in pinned host memory, as the reference's
+    socket/relay path does, through the library's host pipeline (enet_pipeline_aead_*: chunks
+    of --chunk-mib on --streams HIP streams, H2D -> kernel -> D2H overlapped).  Keys, nonces and
+    tags live on the host too and travel with their chunk."""
     import torch
 
     import ephemeralnet_amd as E
 
-    dev = torch.device("cuda", 0)
-    n, L, m = args.records, args.record_bytes, args.chunk_records
-    assert n % m == 0
-    S = 3
+    n, L = args.records, args.record_bytes
     g = torch.Generator().manual_seed(7)
     pt_h = torch.randint(0, 256, (n * L,), dtype=torch.uint8, generator=g).pin_memory()
+    keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
     nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
+    offs_h = torch.arange(0, (n + 1) * L, L, dtype=torch.int64).pin_memory()
     ct_h = torch.empty_like(pt_h).pin_memory()
     back_h = torch.empty_like(pt_h).pin_memory()
     tags_h = torch.empty(16 * n, dtype=torch.uint8).pin_memory()
     ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
-    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev)
-    offs = torch.arange(0, (m + 1) * L, L, dtype=torch.int64, device=dev)
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    din = [torch.empty(m * L, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dout = [torch.empty(m * L, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dn = [torch.empty(m * 12, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dt = [torch.empty(m * 16, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dok = [torch.empty(m, dtype=torch.uint8, device=dev) for _ in range(S)]
-
-    def run(kind):
-        for c in range(n // m):
-            s = c % S
-            st = streams[s]
-            r0, r1 = c * m, (c + 1) * m
-            with torch.cuda.stream(st):
-                src = pt_h if kind == "seal" else ct_h
-                din[s].copy_(src[r0 * L:r1 * L], non_blocking=True)
-                dn[s].copy_(nonces_h[r0 * 12:r1 * 12], non_blocking=True)
-                b = E.Batch(din[s], offs, keys[r0 * 32:r1 * 32], dn[s], total_bytes_hint=m * L,
-                            max_len_hint=L)
-                if kind == "seal":
-                    E.aead_seal(b, dout[s], dt[s], stream=st)
-                    ct_h[r0 * L:r1 * L].copy_(dout[s], non_blocking=True)
-                    tags_h[r0 * 16:r1 * 16].copy_(dt[s], non_blocking=True)
-                else:
-                    dt[s].copy_(tags_h[r0 * 16:r1 * 16], non_blocking=True)
-                    E.aead_open(b, dout[s], dt[s], dok[s], stream=st)
-                    back_h[r0 * L:r1 * L].copy_(dout[s], non_blocking=True)
-                    ok_h[r0:r1].copy_(dok[s], non_blocking=True)
-        torch.cuda.synchronize(dev)
-
-    run("seal")
-    run("open")  # warm-up pass of both directions
+    seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
+    open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
+    pipe = E.Pipeline(0, args.chunk_mib << 20, args.streams)
+    pipe.aead_seal(seal_b, ct_h, tags_h)  # warm-up (grows the pipeline's buffers)
+    pipe.aead_open(open_b, back_h, tags_h, ok_h)
+    reps = 3
     t0 = time.perf_counter()
-    run("seal")
+    for _ in range(reps):
+        pipe.aead_seal(seal_b, ct_h, tags_h)
     t1 = time.perf_counter()
-    run("open")
+    for _ in range(reps):
+        pipe.aead_open(open_b, back_h, tags_h, ok_h)
     t2 = time.perf_counter()
+    pipe.close()
     assert int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
-    gib = n * L / 2**30
+    gib = n * L * reps / 2**30
     return {
         "metric": "GiB/s ChaCha20-Poly1305 seal+open, host-resident (H2D + kernel + D2H)",
         "value": round(gib / (t2 - t0), 2),
         "unit": "GiB/s",
         "seal_GiBs": round(gib / (t1 - t0), 2),
         "open_GiBs": round(gib / (t2 - t1), 2),
-        "config": {"records": n, "record_bytes": L, "chunk_records": m, "streams": S,
-                   "host_buffers": "pinned", "keys": "device-resident", "nonces": "H2D"},
+        "pcie_bytes_per_plaintext_byte": 2.0,
+        "config": {"records": n, "record_bytes": L, "chunk_mib": args.chunk_mib,
+                   "streams": args.streams, "host_buffers": "pinned",
+                   "path": "enet_pipeline_aead_seal/open (libenet_crypto.so)"},
     }
 
 
 def c5(args) -> dict:
-    """Mixed-size batch with the fused HMAC-SHA256 tag, starting and ending in pinned host
-    memory.  Chunks of ~64 MiB go H2D -> aead_hmac_seal -> D2H (then the open direction) on 3
-    streams; inside a chunk records are processed longest-first (`order`) so waves stay balanced.
-    Multi-GPU: each rank takes a byte-balanced contiguous share (shard.py), no collective."""
+    """mixed log-uniform 512 B-64 KiB records with the fused HMAC-SHA256 tag,
+    starting and ending in pinned host memory, through the library's host pipeline
+    (enet_pipeline_aead_hmac_*).  Multi-GPU: each rank takes a byte-balanced contiguous share
+    (shard.py), no collective."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -220,71 +206,31 @@ def c5(args) -> dict:
     lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
     lens = lens_all[lo:hi]
     n = len(lens)
-    offs_h = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    offs_h = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).pin_memory()
     total = int(offs_h[-1])
     g = torch.Generator().manual_seed(11 + rank)
     pt_h = torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g).pin_memory()
+    keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
+    nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
     ct_h = torch.empty_like(pt_h).pin_memory()
     back_h = torch.empty_like(pt_h).pin_memory()
-    nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
     tags_h = torch.empty(16 * n, dtype=torch.uint8).pin_memory()
     macs_h = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
     ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
-    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev)
-    # chunks of ~64 MiB on record boundaries
-    target = 64 << 20
-    cuts = [0]
-    while cuts[-1] < n:
-        k = int(np.searchsorted(offs_h, offs_h[cuts[-1]] + target, side="left"))
-        cuts.append(max(cuts[-1] + 1, min(k, n)))
-    chunks = []
-    for c0, c1 in zip(cuts[:-1], cuts[1:]):
-        o = offs_h[c0:c1 + 1] - offs_h[c0]
-        order = np.argsort(-lens[c0:c1], kind="stable").astype(np.int32)
-        chunks.append((c0, c1, torch.tensor(o, device=dev), torch.tensor(order, device=dev),
-                       int(o[-1]), int(lens[c0:c1].max())))
-    S = 3
-    streams = [torch.cuda.Stream(dev) for _ in range(S)]
-    cap = max(c[4] for c in chunks)
-    mrec = max(c[1] - c[0] for c in chunks)
-    din = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dout = [torch.empty(cap, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dn = [torch.empty(12 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dt = [torch.empty(16 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dm = [torch.empty(32 * mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
-    dok = [torch.empty(mrec, dtype=torch.uint8, device=dev) for _ in range(S)]
+    mx = int(lens.max()) if n else 0
+    seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
+    open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
+    pipe = E.Pipeline(local, args.c5_chunk_mib << 20, args.streams)
 
-    def run(kind):
-        for ci, (c0, c1, o, order, nbytes, mx) in enumerate(chunks):
-            s = ci % S
-            st = streams[s]
-            b0, b1 = int(offs_h[c0]), int(offs_h[c1])
-            m = c1 - c0
-            with torch.cuda.stream(st):
-                din[s][:nbytes].copy_((pt_h if kind == "seal" else ct_h)[b0:b1], non_blocking=True)
-                dn[s][:12 * m].copy_(nonces_h[12 * c0:12 * c1], non_blocking=True)
-                bt = E.Batch(din[s], o, keys[32 * c0:32 * c1], dn[s], order=order,
-                             total_bytes_hint=nbytes, max_len_hint=mx)
-                if kind == "seal":
-                    E.aead_hmac_seal(bt, dout[s], dt[s], dm[s], stream=st)
-                    ct_h[b0:b1].copy_(dout[s][:nbytes], non_blocking=True)
-                    tags_h[16 * c0:16 * c1].copy_(dt[s][:16 * m], non_blocking=True)
-                    macs_h[32 * c0:32 * c1].copy_(dm[s][:32 * m], non_blocking=True)
-                else:
-                    dt[s][:16 * m].copy_(tags_h[16 * c0:16 * c1], non_blocking=True)
-                    dm[s][:32 * m].copy_(macs_h[32 * c0:32 * c1], non_blocking=True)
-                    E.aead_hmac_open(bt, dout[s], dt[s], dm[s], dok[s], stream=st)
-                    back_h[b0:b1].copy_(dout[s][:nbytes], non_blocking=True)
-                    ok_h[c0:c1].copy_(dok[s][:m], non_blocking=True)
-        torch.cuda.synchronize(dev)
+    def step():
+        pipe.aead_hmac_seal(seal_b, ct_h, tags_h, macs_h)
+        pipe.aead_hmac_open(open_b, back_h, tags_h, macs_h, ok_h)
 
-    run("seal")
-    run("open")
+    step()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    run("seal")
-    run("open")
+    step()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -292,6 +238,7 @@ def c5(args) -> dict:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    pipe.close()
     assert int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
     res = None
     if rank == 0:
@@ -302,7 +249,9 @@ def c5(args) -> dict:
             "unit": "GiB/s",
             "n_gpus": world,
             "config": {"workload": "C5", "records_total": n_all, "bytes_total": int(lens_all.sum()),
-                       "chunk_bytes": target, "streams": S, "host_buffers": "pinned"},
+                       "chunk_mib": args.c5_chunk_mib, "streams": args.streams,
+                       "host_buffers": "pinned",
+                       "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
     if world > 1:
         dist.destroy_process_group()
@@ -432,6 +381,23 @@ def main():
         traffic = None
         pmc_note = None
         valu = None
+        dom_s = (seal_ms if dom == "seal" else open_ms) * 1e-3
+        blocks = n * ((L + 63) // 64)
+        if args.mode in ("aead", "xor") and os.path.exists(VALU_CEILING_FILE):
+            with open(VALU_CEILING_FILE) as f:
+                ceil = json.load(f)
+            key = "seal_open_stage_Gblocks_per_s" if args.mode == "aead" else "xor_stage_Gblocks_per_s"
+            peak = ceil[key]["2_waves_per_simd"]
+            achieved = blocks / dom_s / 1e9
+            valu = {
+                "achieved": round(achieved, 2),
+                "peak": peak,
+                "unit": "G ChaCha20 blocks/s (64 B) incl. Poly1305" if args.mode == "aead"
+                        else "G ChaCha20 blocks/s (64 B)",
+                "frac": round(achieved / peak, 4),
+                "peak_is": "compute-only rate of the same stage body, no memory "
+                           "(tools/ubench_seal.hip; " + os.path.relpath(VALU_CEILING_FILE, ROOT) + ")",
+            }
         if os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
@@ -441,20 +407,17 @@ def main():
             if k and args.mode == "aead" and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
                 pmc_note = os.path.relpath(PMC_FILE, ROOT)
-                if "SQ_INSTS_VALU" in k:
-                    # lane-ops per launch from the PMC instruction count, over the kernel time
-                    # measured live above
+                if "SQ_INSTS_VALU" in k and valu is not None:
+                    # wave64 VALU instructions per launch (PMC) over the kernel time measured
+                    # live above: lane-ops/s against the full-rate issue peak, and cycles per
+                    # instruction per SIMD (2.0 = every slot full-rate and paired)
                     ops = k["SQ_INSTS_VALU"] * 64
-                    dom_s = (seal_ms if dom == "seal" else open_ms) * 1e-3
-                    valu = {
-                        "achieved": round(ops / dom_s / 1e12, 2),
-                        "peak": VALU_PEAK_TOPS,
-                        "unit": "T int32 lane-ops/s",
-                        "frac": round(ops / dom_s / 1e12 / VALU_PEAK_TOPS, 4),
-                        "valu_busy_pmc": round(k.get("valu_busy_frac", 0.0), 4),
-                        "ops_per_64B_block": round(ops / (n * L / 64), 1),
-                        "source": pmc_note,
-                    }
+                    valu["lane_ops_Tps"] = round(ops / dom_s / 1e12, 2)
+                    valu["issue_peak_Tps"] = VALU_ISSUE_PEAK_TOPS
+                    valu["instr_per_64B_block"] = round(ops / 64 / blocks, 1)
+                    valu["cycles_per_instr_per_simd_at_2.4GHz"] = round(
+                        dom_s * 2.4e9 * 1024 / k["SQ_INSTS_VALU"], 2)
+                    valu["pmc_source"] = pmc_note
         out = {
             "metric": METRICS[args.mode],
             "value": round(value, 2),
@@ -491,7 +454,7 @@ def main():
                 "traffic": traffic,
                 "traffic_source": pmc_note,
                 "algorithmic_bytes_per_launch": seal_bytes if dom == "seal" else open_bytes,
-                "note": "int32 VALU-bound in practice (~18 ops/B per pass): see valu_roofline",
+                "note": "int32 VALU-issue-bound, not HBM-bound: see valu_roofline",
             },
             "valu_roofline": valu,
         }

@@ -53,7 +53,10 @@ EXPORTS = [
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_last_error",
-    "enet_abi_version",
+    "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
+    "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
+    "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_host_alloc",
+    "enet_host_free",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -90,6 +93,17 @@ def lib() -> C.CDLL:
         L.enet_set_lanes_per_record.argtypes = [u32]
         L.enet_set_staging.argtypes = [C.c_int]
         L.enet_last_error.restype = C.c_char_p
+        L.enet_pipeline_create.argtypes = [C.c_int, u64, u32]
+        L.enet_pipeline_create.restype = vp
+        L.enet_pipeline_destroy.argtypes = [vp]
+        L.enet_pipeline_chacha20_xor.argtypes = [vp, rp, vp]
+        L.enet_pipeline_aead_seal.argtypes = [vp, rp, vp]
+        L.enet_pipeline_aead_open.argtypes = [vp, rp, vp, vp]
+        L.enet_pipeline_aead_hmac_seal.argtypes = [vp, rp, vp, vp]
+        L.enet_pipeline_aead_hmac_open.argtypes = [vp, rp, vp, vp, vp]
+        L.enet_host_alloc.argtypes = [u64]
+        L.enet_host_alloc.restype = vp
+        L.enet_host_free.argtypes = [vp]
         L.enet_abi_version.restype = u32
         for name in EXPORTS:
             getattr(L, name)
@@ -289,3 +303,58 @@ def make_batch(items: Sequence[bytes], keys: Sequence[bytes], nonces: Sequence[b
         total_bytes_hint=total - base_offset,
         max_len_hint=max((len(i) for i in items), default=0),
     )
+
+
+class Pipeline:
+    """Host-resident batches (include/enet_crypto.h "host pipeline"): every tensor of the Batch
+    and every output lives in HOST memory (pinned, e.g. tensor.pin_memory(), for asynchronous
+    DMA); the library cuts the batch into chunks and overlaps H2D, kernels and D2H over several
+    HIP streams.  Calls block until the outputs are in host memory."""
+
+    def __init__(self, device: int = 0, chunk_bytes: int = 0, streams: int = 0):
+        self._p = lib().enet_pipeline_create(device, chunk_bytes, streams)
+        if not self._p:
+            raise EnetError("enet_pipeline_create failed: "
+                            + lib().enet_last_error().decode(errors="replace"))
+
+    def close(self) -> None:
+        if self._p:
+            lib().enet_pipeline_destroy(self._p)
+            self._p = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def chacha20_xor(self, b: Batch, out, counters=None) -> None:
+        r = b.records(out, b.offsets)
+        _check(lib().enet_pipeline_chacha20_xor(self._p, C.byref(r), _ptr(counters)),
+               "enet_pipeline_chacha20_xor")
+
+    def aead_seal(self, b: Batch, out, tags) -> None:
+        r = b.records(out, b.offsets)
+        _check(lib().enet_pipeline_aead_seal(self._p, C.byref(r), _ptr(tags)),
+               "enet_pipeline_aead_seal")
+
+    def aead_open(self, b: Batch, out, tags, ok) -> None:
+        r = b.records(out, b.offsets)
+        _check(lib().enet_pipeline_aead_open(self._p, C.byref(r), _ptr(tags), _ptr(ok)),
+               "enet_pipeline_aead_open")
+
+    def aead_hmac_seal(self, b: Batch, out, tags, macs) -> None:
+        r = b.records(out, b.offsets)
+        _check(lib().enet_pipeline_aead_hmac_seal(self._p, C.byref(r), _ptr(tags), _ptr(macs)),
+               "enet_pipeline_aead_hmac_seal")
+
+    def aead_hmac_open(self, b: Batch, out, tags, macs, ok) -> None:
+        r = b.records(out, b.offsets)
+        _check(lib().enet_pipeline_aead_hmac_open(self._p, C.byref(r), _ptr(tags), _ptr(macs),
+                                                  _ptr(ok)), "enet_pipeline_aead_hmac_open")

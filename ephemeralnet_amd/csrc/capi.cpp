@@ -81,6 +81,8 @@ uint32_t lanes_for(const enet_records* r) {
 
 namespace enet {
 
+void set_last_error(const std::string& what) { g_last_error = what; }
+
 static std::atomic<uint32_t> g_forced_lanes{0};
 static std::atomic<uint32_t> g_staging{0};
 

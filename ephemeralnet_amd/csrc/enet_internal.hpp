@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace enet {
 
 constexpr int kWG = 256;           // threads per workgroup (4 waves of 64)
@@ -71,5 +73,7 @@ hipError_t launch_sha(const ShaParams& p, hipStream_t s);
 
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
 uint32_t staging_variant();
+// the text enet_last_error() returns on this host thread
+void set_last_error(const std::string& what);
 
 }  // namespace enet

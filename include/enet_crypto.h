@@ -147,6 +147,42 @@ ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_
 ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
                                     const uint8_t* chunk_hashes, uint8_t* ok, void* stream);
 
+/* ---- host-resident pipeline
+ * The reference's crypto path starts and ends in host memory (socket / relay buffers,
+ * SessionManager.cpp:362-387 and 815-822; chunk files, Node.cpp:1414-1417 and 1641-1655).  These
+ * calls take an enet_records batch whose arenas, offsets, keys, nonces, counters, tags, MACs and
+ * ok flags are all HOST pointers, cut it into chunks of about `chunk_bytes` on record boundaries
+ * and run H2D -> kernel(s) -> D2H per chunk on `streams` HIP streams, so copies of one chunk
+ * overlap the kernels and copies of the others; inside a chunk of mixed lengths records are run
+ * longest first.  Arenas from enet_host_alloc (pinned) move by
+ * asynchronous DMA; pageable arenas work but each of their copies blocks the calling thread.
+ * Records keep their length (in/out offsets describe equal-length records); `order` must be
+ * NULL.  Every call blocks until all outputs are in host memory.  A pipeline owns its streams
+ * and device / pinned staging buffers (grown on demand) and serves one host thread at a time. */
+typedef struct enet_pipeline enet_pipeline;
+/* device: HIP ordinal; chunk_bytes: 0 = 16 MiB (mixed-length batches with HMAC want larger
+ * chunks: one lane hashes a whole record, so a chunk takes at least its longest record's
+ * serial SHA-256 time); streams: 0 = 3 (max 16).  NULL on failure.  The defaults saturate
+ * PCIe Gen5 on MI355X for uniform batches (~64 GB/s both directions together). */
+ENET_API enet_pipeline* enet_pipeline_create(int device, uint64_t chunk_bytes, uint32_t streams);
+ENET_API void enet_pipeline_destroy(enet_pipeline* pipe);
+/* ChaCha20::apply per record (CryptoManager chunk mode with counters = LE32(chunk_id)) */
+ENET_API int enet_pipeline_chacha20_xor(enet_pipeline* pipe, const enet_records* host_records,
+                                        const uint32_t* counters);
+/* RFC 8439 AEAD seal / open (no AAD): tags [n][16]; ok [n] (failed records come back zeroed) */
+ENET_API int enet_pipeline_aead_seal(enet_pipeline* pipe, const enet_records* host_records,
+                                     uint8_t* tags);
+ENET_API int enet_pipeline_aead_open(enet_pipeline* pipe, const enet_records* host_records,
+                                     const uint8_t* tags, uint8_t* ok);
+/* AEAD + HMAC-SHA256(key, plaintext) (enet_aead_hmac_*_batch): macs [n][32] */
+ENET_API int enet_pipeline_aead_hmac_seal(enet_pipeline* pipe, const enet_records* host_records,
+                                          uint8_t* tags, uint8_t* macs);
+ENET_API int enet_pipeline_aead_hmac_open(enet_pipeline* pipe, const enet_records* host_records,
+                                          const uint8_t* tags, const uint8_t* macs, uint8_t* ok);
+/* Pinned host memory for socket / relay buffer pools (hipHostMalloc); NULL on failure. */
+ENET_API void* enet_host_alloc(uint64_t bytes);
+ENET_API void enet_host_free(void* p);
+
 /* ---- helpers (host) */
 /* LE32(chunk_id[0..3]) -- CryptoManager.cpp:8-13 derive_counter. */
 ENET_API uint32_t enet_chunk_counter(const uint8_t chunk_id[32]);
