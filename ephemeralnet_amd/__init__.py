@@ -11,6 +11,9 @@ Operations mirror the reference src/crypto API, batched (ShardianLabs/EphemeralN
   hmac_sha256    HmacSha256::compute/verify src/crypto/HmacSha256.cpp:11-54
   frame_seal/open encode_signed + SessionManager frame body
                   src/protocol/Message.cpp:305-328, src/network/SessionManager.cpp:362-374,815-822
+  pow_search/check compute_store_pow / compute_{announce,handshake}_pow and the *_valid checks
+                  src/security/StoreProof.cpp:109-146, src/core/Node.cpp:193-292
+  session_keys   KeyManager::derive_key     src/network/KeyManager.cpp:74-92
 """
 from __future__ import annotations
 
@@ -56,8 +59,11 @@ EXPORTS = [
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
     "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_host_alloc",
-    "enet_host_free",
+    "enet_host_free", "enet_pow_search_batch", "enet_pow_check_batch", "enet_session_key_batch",
 ]
+
+POW_NODE = 0   # candidates start + attempt (Node.cpp announce / handshake)
+POW_STORE = 1  # candidates = successive mt19937_64 outputs (StoreProof.cpp)
 
 _lib: Optional[C.CDLL] = None
 
@@ -105,6 +111,9 @@ def lib() -> C.CDLL:
         L.enet_host_alloc.restype = vp
         L.enet_host_free.argtypes = [vp]
         L.enet_abi_version.restype = u32
+        L.enet_pow_search_batch.argtypes = [u32, vp, vp, vp, C.c_int, u64, vp, vp, vp, vp]
+        L.enet_pow_check_batch.argtypes = [u32, vp, vp, vp, vp, vp, vp]
+        L.enet_session_key_batch.argtypes = [u32, vp, vp, vp, vp, vp]
         for name in EXPORTS:
             getattr(L, name)
         _lib = L
@@ -256,6 +265,33 @@ def chunk_fetch(b: Batch, out, chunk_ids, chunk_hashes, ok, stream=None) -> None
     r = b.records(out, b.offsets)
     _check(lib().enet_chunk_fetch_batch(C.byref(r), _ptr(chunk_ids), _ptr(chunk_hashes), _ptr(ok),
                                         _stream(stream)), "enet_chunk_fetch_batch")
+
+
+def pow_search(prefixes, offsets, difficulty, schedule: int, max_attempts: int, nonces, found,
+               attempts=None, stream=None) -> None:
+    """First nonce (attempt order) with >= difficulty leading zero bits of
+    SHA-256(prefix || BE64(nonce)); schedule POW_NODE or POW_STORE.  Device tensors: prefixes
+    uint8 arena, offsets int64 [n+1], difficulty uint8 [n], nonces/attempts int64 [n], found
+    uint8 [n]."""
+    n = int(offsets.numel()) - 1
+    _check(lib().enet_pow_search_batch(n, _ptr(prefixes), _ptr(offsets), _ptr(difficulty), schedule,
+                                       max_attempts, _ptr(nonces), _ptr(attempts), _ptr(found),
+                                       _stream(stream)), "enet_pow_search_batch")
+
+
+def pow_check(prefixes, offsets, nonces, difficulty, ok, stream=None) -> None:
+    n = int(offsets.numel()) - 1
+    _check(lib().enet_pow_check_batch(n, _ptr(prefixes), _ptr(offsets), _ptr(nonces),
+                                      _ptr(difficulty), _ptr(ok), _stream(stream)),
+           "enet_pow_check_batch")
+
+
+def session_keys(secrets, counters, ticks, out, stream=None) -> None:
+    """KeyManager::derive_key for n sessions: out[i] = HMAC(secrets[i], BE64(counters[i]) ||
+    BE64(ticks[i])).  secrets uint8 [n*32], counters/ticks int64 [n], out uint8 [n*32]."""
+    n = int(counters.numel())
+    _check(lib().enet_session_key_batch(n, _ptr(secrets), _ptr(counters), _ptr(ticks), _ptr(out),
+                                        _stream(stream)), "enet_session_key_batch")
 
 
 def chunk_counter(chunk_id: bytes) -> int:

@@ -129,7 +129,7 @@ uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len) {
 
 extern "C" {
 
-uint32_t enet_abi_version(void) { return (1u << 16) | 0u; }
+uint32_t enet_abi_version(void) { return (1u << 16) | 1u; }
 
 const char* enet_last_error(void) { return g_last_error.c_str(); }
 
@@ -444,6 +444,63 @@ int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void
     s.zero_on_fail = r->out;
     s.order = r->order;
     return hip_status(enet::launch_sha(s, st), "wire_open hmac verify");
+}
+
+int enet_pow_search_batch(uint32_t n, const uint8_t* prefixes, const uint64_t* prefix_offsets,
+                          const uint8_t* difficulty, int schedule, uint64_t max_attempts,
+                          uint64_t* nonces, uint64_t* attempts, uint8_t* found, void* stream) {
+    if (n == 0) return ENET_OK;
+    if (!prefixes || !prefix_offsets || !difficulty || !nonces || !found)
+        return fail(ENET_EINVAL, "pow_search: NULL argument");
+    if (schedule != ENET_POW_NODE && schedule != ENET_POW_STORE)
+        return fail(ENET_EINVAL, "pow_search: schedule must be ENET_POW_NODE or ENET_POW_STORE");
+    if (n > 0x7FFFFFFFu) return fail(ENET_EINVAL, "pow_search: too many jobs");
+    // one workgroup per job: enough waves per job that the grid holds ~4 waves per SIMD
+    // (1024 SIMDs), at most 16 (1024 threads), never more lanes than attempts
+    uint32_t waves = 1;
+    while (waves < 16 && (uint64_t)n * waves < 4096 && 64ull * waves < max_attempts) waves <<= 1;
+    enet::PowParams p{};
+    p.n = n;
+    p.prefixes = prefixes;
+    p.off = prefix_offsets;
+    p.difficulty = difficulty;
+    p.schedule = (uint32_t)schedule;
+    p.max_attempts = max_attempts;
+    if (schedule == ENET_POW_STORE) {
+        uint64_t r = 1;
+        while (r < 64ull * waves + 312) r <<= 1;
+        p.ring = r;
+    }
+    p.nonces = nonces;
+    p.attempts = attempts;
+    p.found = found;
+    return hip_status(enet::launch_pow_search(p, waves, (hipStream_t)stream), "pow_search launch");
+}
+
+int enet_pow_check_batch(uint32_t n, const uint8_t* prefixes, const uint64_t* prefix_offsets,
+                         const uint64_t* nonces, const uint8_t* difficulty, uint8_t* ok,
+                         void* stream) {
+    if (n == 0) return ENET_OK;
+    if (!prefixes || !prefix_offsets || !nonces || !difficulty || !ok)
+        return fail(ENET_EINVAL, "pow_check: NULL argument");
+    enet::PowParams p{};
+    p.n = n;
+    p.prefixes = prefixes;
+    p.off = prefix_offsets;
+    p.difficulty = difficulty;
+    p.check_nonces = nonces;
+    p.found = ok;
+    return hip_status(enet::launch_pow_check(p, (hipStream_t)stream), "pow_check launch");
+}
+
+int enet_session_key_batch(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
+                           const int64_t* ticks, uint8_t* keys_out, void* stream) {
+    if (n == 0) return ENET_OK;
+    if (!secrets || !counters || !ticks || !keys_out)
+        return fail(ENET_EINVAL, "session_key: NULL argument");
+    return hip_status(enet::launch_session_keys(n, secrets, counters, ticks, keys_out,
+                                                (hipStream_t)stream),
+                      "session_key launch");
 }
 
 }  // extern "C"

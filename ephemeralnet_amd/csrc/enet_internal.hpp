@@ -70,6 +70,26 @@ struct ShaParams {
 };
 hipError_t launch_sha(const ShaParams& p, hipStream_t s);
 
+// Proof-of-work search / check (pow.hip): SHA-256(prefix_i || BE64(candidate)).
+struct PowParams {
+    uint32_t n;
+    const uint8_t* prefixes;
+    const uint64_t* off;
+    const uint8_t* difficulty;     // per job, 0 -> nonce 0 / valid
+    uint32_t schedule;             // 0 = start + attempt (Node.cpp), 1 = mt19937_64 stream (StoreProof.cpp)
+    uint64_t max_attempts;
+    uint64_t ring;                 // LDS candidate ring (power of two >= 64*waves + 312; 0 for schedule 0)
+    uint64_t* nonces;              // search: found nonce
+    uint64_t* attempts;            // search: attempt index of the nonce (nullable)
+    uint8_t* found;                // search: found flag; check: valid flag
+    const uint64_t* check_nonces;  // check: nonce per job
+};
+hipError_t launch_pow_search(const PowParams& p, uint32_t waves, hipStream_t s);
+hipError_t launch_pow_check(const PowParams& p, hipStream_t s);
+
+// KeyManager::derive_key for many sessions (sha.hip)
+hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
+                               const int64_t* ticks, uint8_t* out, hipStream_t s);
 
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
 uint32_t staging_variant();

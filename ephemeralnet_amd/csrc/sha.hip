@@ -169,4 +169,56 @@ hipError_t launch_sha(const ShaParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// KeyManager::derive_key (src/network/KeyManager.cpp:74-92): HMAC-SHA256 with the 32-byte shared
+// secret over the 16-byte material BE64(counter) || BE64(ticks) -- four compressions per
+// session (ipad, inner message, opad, outer), one session per lane.
+__global__ __launch_bounds__(kWG) void session_key_kernel(uint32_t n, const uint8_t* __restrict__ secrets,
+                                                          const uint64_t* __restrict__ counters,
+                                                          const int64_t* __restrict__ ticks,
+                                                          uint8_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= n) return;
+    const uint4* kq = reinterpret_cast<const uint4*>(secrets + 32ull * i);
+    const uint4 k0 = kq[0], k1 = kq[1];
+    const uint32_t kb[8] = {bswap32(k0.x), bswap32(k0.y), bswap32(k0.z), bswap32(k0.w),
+                            bswap32(k1.x), bswap32(k1.y), bswap32(k1.z), bswap32(k1.w)};
+    const uint64_t c = counters[i], t = (uint64_t)ticks[i];
+    uint32_t st[8], w[16];
+    sha_init(st);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = (j < 8 ? kb[j] : 0u) ^ 0x36363636u;
+    sha256_compress(st, w);
+    w[0] = (uint32_t)(c >> 32); w[1] = (uint32_t)c; w[2] = (uint32_t)(t >> 32); w[3] = (uint32_t)t;
+    w[4] = 0x80000000u;
+#pragma unroll
+    for (int j = 5; j < 15; ++j) w[j] = 0u;
+    w[15] = (64 + 16) * 8;
+    sha256_compress(st, w);
+    uint32_t inner[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) inner[j] = st[j];
+    sha_init(st);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = (j < 8 ? kb[j] : 0u) ^ 0x5c5c5c5cu;
+    sha256_compress(st, w);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = inner[j];
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int j = 9; j < 15; ++j) w[j] = 0u;
+    w[15] = (64 + 32) * 8;
+    sha256_compress(st, w);
+    uint4* o = reinterpret_cast<uint4*>(out + 32ull * i);
+    o[0] = make_uint4(bswap32(st[0]), bswap32(st[1]), bswap32(st[2]), bswap32(st[3]));
+    o[1] = make_uint4(bswap32(st[4]), bswap32(st[5]), bswap32(st[6]), bswap32(st[7]));
+}
+
+hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
+                               const int64_t* ticks, uint8_t* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(session_key_kernel, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s, n, secrets,
+                       counters, ticks, out);
+    return hipGetLastError();
+}
+
 }  // namespace enet

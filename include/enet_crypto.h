@@ -147,6 +147,40 @@ ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_
 ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
                                     const uint8_t* chunk_hashes, uint8_t* ok, void* stream);
 
+/* ---- proof of work
+ * Every PoW in the reference hashes SHA-256(prefix || BE64(candidate)) and accepts the FIRST
+ * candidate, in attempt order, whose digest has >= difficulty leading zero bits:
+ *   ENET_POW_NODE  (0): compute_announce_pow / compute_handshake_pow (src/core/Node.cpp:212-230,
+ *                       269-292): candidate(a) = start + a, start = first std::mt19937_64 output
+ *                       seeded with BE64(SHA-256(prefix || BE64(0))[0..8]) (:200-209, :247-256);
+ *   ENET_POW_STORE (1): security::compute_store_pow (src/security/StoreProof.cpp:124-146):
+ *                       candidate(a) = a-th std::mt19937_64 output seeded with
+ *                       LE64(SHA-256(prefix || BE64(0))[0..8]).
+ * Prefix serialisations: StoreProof.cpp:39-52 (chunk_id || BE64 size || BE32 len || hint) and
+ * Node.cpp:155-171 / 233-245 (BE64-length-prefixed fields); see crypto::batch::*_pow_prefix.
+ * prefixes/prefix_offsets: arena + [n+1] offsets; difficulty: [n] bits (0 -> nonce 0, found;
+ * callers clamp as the reference does, StoreProof.cpp:128-130).  Outputs: nonces [n],
+ * attempts [n] (nullable: index of the nonce in attempt order, or max_attempts), found [n]. */
+#define ENET_POW_NODE 0
+#define ENET_POW_STORE 1
+ENET_API int enet_pow_search_batch(uint32_t n, const uint8_t* prefixes,
+                                   const uint64_t* prefix_offsets, const uint8_t* difficulty,
+                                   int schedule, uint64_t max_attempts, uint64_t* nonces,
+                                   uint64_t* attempts, uint8_t* found, void* stream);
+/* store_pow_valid / announce_pow_valid / handshake_pow_valid (StoreProof.cpp:109-121,
+ * Node.cpp:193-198, 247-255) without the clamp: ok[i] = lzb(SHA-256(prefix_i || BE64(nonces[i])))
+ * >= difficulty[i] (difficulty 0 -> 1). */
+ENET_API int enet_pow_check_batch(uint32_t n, const uint8_t* prefixes,
+                                  const uint64_t* prefix_offsets, const uint64_t* nonces,
+                                  const uint8_t* difficulty, uint8_t* ok, void* stream);
+
+/* ---- session key derivation
+ * network::KeyManager::derive_key (src/network/KeyManager.cpp:74-92) for n sessions:
+ * keys_out[i] = HMAC-SHA256(secrets[i], BE64(counters[i]) || BE64(ticks[i])), ticks = the
+ * rotation time in ns since the steady_clock epoch (register_session uses counter 0, :15-30). */
+ENET_API int enet_session_key_batch(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
+                                    const int64_t* ticks, uint8_t* keys_out, void* stream);
+
 /* ---- host-resident pipeline
  * The reference's crypto path starts and ends in host memory (socket / relay buffers,
  * SessionManager.cpp:362-387 and 815-822; chunk files, Node.cpp:1414-1417 and 1641-1655).  These

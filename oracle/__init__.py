@@ -43,6 +43,25 @@ def lib() -> C.CDLL:
         _lib.orc_derive_counter.argtypes = [p]
         _lib.orc_derive_counter.restype = C.c_uint32
         _lib.orc_bench_aead.argtypes = [C.c_void_p] * 6 + [sz, sz, C.c_int, C.c_void_p]
+        u64 = C.c_uint64
+        _lib.orc_mt64_seed.argtypes = [C.c_void_p, u64]
+        _lib.orc_mt64_next.argtypes = [C.c_void_p]
+        _lib.orc_mt64_next.restype = u64
+        _lib.orc_pow_digest.argtypes = [p, sz, u64, C.c_void_p]
+        _lib.orc_leading_zero_bits.argtypes = [p]
+        _lib.orc_leading_zero_bits.restype = C.c_uint
+        _lib.orc_store_pow_prefix.argtypes = [p, u64, p, sz, C.c_void_p]
+        _lib.orc_store_pow_prefix.restype = sz
+        _lib.orc_announce_pow_prefix.argtypes = [p, p, p, sz, p, sz, p, sz, C.c_int64, C.c_void_p]
+        _lib.orc_announce_pow_prefix.restype = sz
+        _lib.orc_handshake_pow_prefix.argtypes = [p, p, C.c_uint32, C.c_void_p]
+        _lib.orc_handshake_pow_prefix.restype = sz
+        _lib.orc_pow_search.argtypes = [p, sz, C.c_uint, C.c_int, u64, C.POINTER(u64), C.POINTER(u64)]
+        _lib.orc_pow_check.argtypes = [p, sz, u64, C.c_uint]
+        _lib.orc_session_key.argtypes = [p, u64, C.c_int64, C.c_void_p]
+        _lib.orc_bench_pow.argtypes = [C.c_void_p, C.c_void_p, sz, C.c_uint, u64, C.c_int,
+                                       C.POINTER(u64)]
+        _lib.orc_bench_pow.restype = C.c_double
     return _lib
 
 
@@ -117,3 +136,62 @@ def frame_open(key: bytes, nonce: bytes, body: bytes):
 
 def derive_counter(chunk_id: bytes) -> int:
     return int(lib().orc_derive_counter(chunk_id))
+
+
+# ------------------------------------------------------------------ proof of work / session keys
+class _MT64(C.Structure):
+    _fields_ = [("mt", C.c_uint64 * 312), ("mti", C.c_int)]
+
+
+def mt19937_64(seed: int, n: int) -> list:
+    g = _MT64()
+    lib().orc_mt64_seed(C.byref(g), seed & 0xFFFFFFFFFFFFFFFF)
+    return [lib().orc_mt64_next(C.byref(g)) for _ in range(n)]
+
+
+def leading_zero_bits(digest: bytes) -> int:
+    return int(lib().orc_leading_zero_bits(digest))
+
+
+def pow_digest(prefix: bytes, nonce: int) -> bytes:
+    o = _buf(32)
+    lib().orc_pow_digest(prefix, len(prefix), nonce & 0xFFFFFFFFFFFFFFFF, o)
+    return bytes(o)
+
+
+def store_pow_prefix(chunk_id: bytes, payload_size: int, hint: bytes = b"") -> bytes:
+    o = _buf(64 + len(hint))
+    n = lib().orc_store_pow_prefix(chunk_id, payload_size, hint, len(hint), o)
+    return bytes(o)[:n]
+
+
+def announce_pow_prefix(chunk_id: bytes, peer_id: bytes, endpoint: bytes, uri: bytes,
+                        shards: bytes, ttl: int) -> bytes:
+    o = _buf(120 + len(endpoint) + len(uri) + len(shards))
+    n = lib().orc_announce_pow_prefix(chunk_id, peer_id, endpoint, len(endpoint), uri, len(uri),
+                                      shards, len(shards), ttl, o)
+    return bytes(o)[:n]
+
+
+def handshake_pow_prefix(initiator: bytes, responder: bytes, public: int) -> bytes:
+    o = _buf(96)
+    n = lib().orc_handshake_pow_prefix(initiator, responder, public, o)
+    return bytes(o)[:n]
+
+
+def pow_search(prefix: bytes, difficulty: int, schedule: int, max_attempts: int):
+    """(found, nonce, attempt) -- schedule 0 = Node.cpp announce/handshake, 1 = StoreProof.cpp."""
+    nonce, att = C.c_uint64(), C.c_uint64()
+    f = lib().orc_pow_search(prefix, len(prefix), difficulty, schedule, max_attempts,
+                             C.byref(nonce), C.byref(att))
+    return bool(f), nonce.value, att.value
+
+
+def pow_check(prefix: bytes, nonce: int, difficulty: int) -> bool:
+    return bool(lib().orc_pow_check(prefix, len(prefix), nonce & 0xFFFFFFFFFFFFFFFF, difficulty))
+
+
+def session_key(secret: bytes, counter: int, ticks: int) -> bytes:
+    o = _buf(32)
+    lib().orc_session_key(secret, counter & 0xFFFFFFFFFFFFFFFF, ticks, o)
+    return bytes(o)

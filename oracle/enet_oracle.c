@@ -359,6 +359,137 @@ int orc_frame_open(const uint8_t key[32], const uint8_t nonce[12], const uint8_t
     return ok;
 }
 
+/* ------------------------------------------------------------ proof of work */
+void orc_mt64_seed(orc_mt64* g, uint64_t seed) { /* std::mersenne_twister_engine::seed */
+    g->mt[0] = seed;
+    for (int i = 1; i < 312; ++i)
+        g->mt[i] = 6364136223846793005ull * (g->mt[i - 1] ^ (g->mt[i - 1] >> 62)) + (uint64_t)i;
+    g->mti = 312;
+}
+
+uint64_t orc_mt64_next(orc_mt64* g) {
+    if (g->mti >= 312) { /* twist, in place, index order */
+        for (int i = 0; i < 312; ++i) {
+            const uint64_t x = (g->mt[i] & 0xFFFFFFFF80000000ull) | (g->mt[(i + 1) % 312] & 0x7FFFFFFFull);
+            g->mt[i] = g->mt[(i + 156) % 312] ^ (x >> 1) ^ ((x & 1u) ? 0xB5026F5AA96619E9ull : 0ull);
+        }
+        g->mti = 0;
+    }
+    uint64_t y = g->mt[g->mti++];
+    y ^= (y >> 29) & 0x5555555555555555ull;
+    y ^= (y << 17) & 0x71D67FFFEDA60000ull;
+    y ^= (y << 37) & 0xFFF7EEE000000000ull;
+    y ^= y >> 43;
+    return y;
+}
+
+unsigned orc_leading_zero_bits(const uint8_t d[32]) { /* Node.cpp:174-190 */
+    unsigned total = 0;
+    for (int i = 0; i < 32; ++i) {
+        if (d[i] == 0) { total += 8; continue; }
+        for (int bit = 7; bit >= 0; --bit) {
+            if ((d[i] >> bit) & 1u) return total;
+            ++total;
+        }
+    }
+    return total;
+}
+
+static void be64(uint8_t* p, uint64_t v) {
+    for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+void orc_pow_digest(const uint8_t* prefix, size_t plen, uint64_t nonce, uint8_t out[32]) {
+    sha_ctx c;
+    uint8_t nb[8];
+    sha_init(&c);
+    sha_update(&c, prefix, plen);
+    be64(nb, nonce); /* to_big_endian(nonce), StoreProof.cpp:50 / Node.cpp:168 */
+    sha_update(&c, nb, 8);
+    sha_final(&c, out);
+}
+
+size_t orc_store_pow_prefix(const uint8_t chunk_id[32], uint64_t payload_size, const uint8_t* hint,
+                            size_t hint_len, uint8_t* out) {
+    size_t o = 0;
+    memcpy(out, chunk_id, 32); o += 32;          /* :41 */
+    be64(out + o, payload_size); o += 8;         /* :42 */
+    const uint32_t l = hint_len > 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)hint_len; /* :26 */
+    out[o++] = (uint8_t)(l >> 24); out[o++] = (uint8_t)(l >> 16);
+    out[o++] = (uint8_t)(l >> 8); out[o++] = (uint8_t)l;
+    if (hint_len) { memcpy(out + o, hint, hint_len); o += hint_len; }
+    return o;
+}
+
+static size_t lp64(uint8_t* out, const uint8_t* p, size_t n) { /* Node.cpp:149-153 */
+    be64(out, (uint64_t)n);
+    if (n) memcpy(out + 8, p, n);
+    return 8 + n;
+}
+
+size_t orc_announce_pow_prefix(const uint8_t chunk_id[32], const uint8_t peer_id[32],
+                               const uint8_t* endpoint, size_t elen, const uint8_t* uri,
+                               size_t ulen, const uint8_t* shards, size_t slen, int64_t ttl,
+                               uint8_t* out) {
+    size_t o = 0;
+    o += lp64(out + o, chunk_id, 32);
+    o += lp64(out + o, peer_id, 32);
+    o += lp64(out + o, endpoint, elen);
+    o += lp64(out + o, uri, ulen);
+    o += lp64(out + o, shards, slen);
+    be64(out + o, (uint64_t)ttl); o += 8; /* Node.cpp:165-166 */
+    return o;
+}
+
+size_t orc_handshake_pow_prefix(const uint8_t initiator[32], const uint8_t responder[32],
+                                uint32_t initiator_public, uint8_t* out) {
+    size_t o = 0;
+    o += lp64(out + o, initiator, 32);
+    o += lp64(out + o, responder, 32);
+    be64(out + o, (uint64_t)initiator_public); o += 8; /* Node.cpp:241-242 */
+    return o;
+}
+
+int orc_pow_check(const uint8_t* prefix, size_t plen, uint64_t nonce, unsigned difficulty) {
+    if (difficulty == 0) return 1;
+    uint8_t d[32];
+    orc_pow_digest(prefix, plen, nonce, d);
+    return orc_leading_zero_bits(d) >= difficulty;
+}
+
+int orc_pow_search(const uint8_t* prefix, size_t plen, unsigned difficulty, int schedule,
+                   uint64_t max_attempts, uint64_t* nonce, uint64_t* attempt) {
+    if (difficulty == 0) { *nonce = 0; *attempt = 0; return 1; }
+    uint8_t d[32];
+    orc_pow_digest(prefix, plen, 0, d);
+    uint64_t seed = 0;
+    if (schedule == 1) { /* memcpy(&seed, digest, 8), StoreProof.cpp:136-137 */
+        for (int i = 7; i >= 0; --i) seed = (seed << 8) | d[i];
+    } else {             /* Node.cpp:205-207 / 261-263 */
+        for (int i = 0; i < 8; ++i) seed = (seed << 8) | d[i];
+    }
+    orc_mt64 g;
+    orc_mt64_seed(&g, seed);
+    const uint64_t start = schedule == 1 ? 0 : orc_mt64_next(&g);
+    for (uint64_t a = 0; a < max_attempts; ++a) {
+        const uint64_t cand = schedule == 1 ? orc_mt64_next(&g) : start + a;
+        if (orc_pow_check(prefix, plen, cand, difficulty)) {
+            *nonce = cand;
+            *attempt = a;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------ session key derivation */
+void orc_session_key(const uint8_t secret[32], uint64_t counter, int64_t ticks, uint8_t out[32]) {
+    uint8_t m[16];
+    be64(m, counter);          /* KeyManager.cpp:79-81 */
+    be64(m + 8, (uint64_t)ticks); /* :83-86 */
+    orc_hmac_sha256(secret, 32, m, 16, out); /* :88-90 */
+}
+
 /* ----------------------------------------------------------- CPU baseline */
 typedef struct {
     const uint8_t *pt, *keys, *nonces;
@@ -414,4 +545,49 @@ int orc_bench_aead(const uint8_t* pt, uint8_t* ct, uint8_t* back, const uint8_t*
     free(th);
     free(jobs);
     return fails;
+}
+
+typedef struct {
+    const uint8_t* prefixes;
+    const uint64_t* off;
+    size_t lo, hi;
+    unsigned difficulty;
+    uint64_t max_attempts, hashes;
+} pow_job;
+
+static void* pow_worker(void* arg) {
+    pow_job* j = (pow_job*)arg;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+        uint64_t nonce = 0, at = 0;
+        const int f = orc_pow_search(j->prefixes + j->off[i], (size_t)(j->off[i + 1] - j->off[i]),
+                                     j->difficulty, 0, j->max_attempts, &nonce, &at);
+        j->hashes += 1 + (f ? at + 1 : j->max_attempts); /* + the seed digest */
+    }
+    return NULL;
+}
+
+double orc_bench_pow(const uint8_t* prefixes, const uint64_t* offsets, size_t jobs,
+                     unsigned difficulty, uint64_t max_attempts, int threads, uint64_t* hashes) {
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
+    pow_job* js = (pow_job*)calloc((size_t)threads, sizeof(pow_job));
+    const double t0 = now_s();
+    for (int t = 0; t < threads; ++t) {
+        pow_job* j = &js[t];
+        j->prefixes = prefixes; j->off = offsets; j->difficulty = difficulty;
+        j->max_attempts = max_attempts;
+        j->lo = jobs * (size_t)t / (size_t)threads;
+        j->hi = jobs * (size_t)(t + 1) / (size_t)threads;
+        pthread_create(&th[t], NULL, pow_worker, j);
+    }
+    uint64_t h = 0;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        h += js[t].hashes;
+    }
+    const double dt = now_s() - t0;
+    free(th);
+    free(js);
+    *hashes = h;
+    return dt;
 }

@@ -9,10 +9,16 @@
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 #include "ephemeralnet/crypto/HmacSha256.hpp"
 #include "ephemeralnet/crypto/Sha256.hpp"
+#include "ephemeralnet/network/KeyManager.hpp"
 #include "ephemeralnet/protocol/Message.hpp"
+#include "ephemeralnet/security/StoreProof.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <limits>
+#include <random>
+#include <string_view>
 
 using namespace ephemeralnet;
 
@@ -113,6 +119,79 @@ int ref_decode_signed_ok(const uint8_t* buf, size_t n, const uint8_t* key, size_
     return protocol::decode_signed(std::span<const uint8_t>(buf, n), std::span<const uint8_t>(key, klen)).has_value()
                ? 1
                : 0;
+}
+
+// security::compute_store_pow / store_pow_valid / derive_chunk_id (src/security/StoreProof.cpp)
+int ref_compute_store_pow(const uint8_t* chunk_id, uint64_t payload_size, const char* hint, size_t hlen,
+                          uint8_t difficulty, uint64_t max_attempts, uint64_t* nonce) {
+    security::StoreWorkInput in{};
+    std::memcpy(in.chunk_id.data(), chunk_id, 32);
+    in.payload_size = payload_size;
+    in.filename_hint = std::string_view(hint, hlen);
+    auto r = security::compute_store_pow(in, difficulty, max_attempts);
+    if (!r) return 0;
+    *nonce = *r;
+    return 1;
+}
+int ref_store_pow_valid(const uint8_t* chunk_id, uint64_t payload_size, const char* hint, size_t hlen,
+                        uint64_t nonce, uint8_t difficulty) {
+    security::StoreWorkInput in{};
+    std::memcpy(in.chunk_id.data(), chunk_id, 32);
+    in.payload_size = payload_size;
+    in.filename_hint = std::string_view(hint, hlen);
+    return security::store_pow_valid(in, nonce, difficulty) ? 1 : 0;
+}
+
+// std::mt19937_64 and the full-range uniform_int_distribution draw Node.cpp:217-220 / 279-282 use
+void ref_mt64(uint64_t seed, size_t n, uint64_t* out) {
+    std::mt19937_64 g(seed);
+    for (size_t i = 0; i < n; ++i) out[i] = g();
+}
+uint64_t ref_mt64_uniform_first(uint64_t seed) {
+    std::mt19937_64 g(seed);
+    std::uniform_int_distribution<std::uint64_t> d(0, std::numeric_limits<std::uint64_t>::max());
+    return d(g);
+}
+
+// Sha256 over arbitrary pieces (used to restate Node.cpp's anonymous-namespace PoW digests with
+// the reference hasher: update_length_prefixed = BE64(len) || data, Node.cpp:149-153)
+void ref_sha256_concat(const uint8_t* const* pieces, const size_t* lens, size_t count, uint8_t* out) {
+    crypto::Sha256 h;
+    for (size_t i = 0; i < count; ++i)
+        if (lens[i]) h.update(std::span<const uint8_t>(pieces[i], lens[i]));
+    auto d = h.finalize();
+    std::memcpy(out, d.data(), 32);
+}
+
+// network::KeyManager (src/network/KeyManager.cpp:33-46): current_key after
+// register_session_with_material = HMAC(shared_secret, material)
+void ref_keymanager_material_key(const uint8_t* secret, const uint8_t* material, size_t mlen, uint8_t* out) {
+    network::KeyManager km;
+    PeerId peer{};
+    peer[0] = 1;
+    crypto::Key k{};
+    std::memcpy(k.bytes.data(), secret, 32);
+    km.register_session_with_material(peer, k, std::span<const uint8_t>(material, mlen),
+                                      std::chrono::steady_clock::time_point{});
+    auto key = km.current_key(peer);
+    std::memcpy(out, key->data(), 32);
+}
+// KeyManager::rotate_if_needed (:56-72) after one interval: derive_key(secret, 1, now) (:74-92).
+// Returns the ticks (ns since the steady_clock epoch) the reference used.
+int64_t ref_keymanager_rotate(const uint8_t* secret, int64_t now_ns, uint8_t* out) {
+    network::KeyManager km(std::chrono::seconds(1));
+    PeerId peer{};
+    peer[0] = 2;
+    crypto::Key k{};
+    std::memcpy(k.bytes.data(), secret, 32);
+    uint8_t material[16] = {};
+    km.register_session_with_material(peer, k, std::span<const uint8_t>(material, 16),
+                                      std::chrono::steady_clock::time_point{});
+    const auto now = std::chrono::steady_clock::time_point{} + std::chrono::nanoseconds(now_ns);
+    auto key = km.rotate_if_needed(peer, now);
+    if (!key) return -1;
+    std::memcpy(out, key->data(), 32);
+    return now_ns;
 }
 
 }  // extern "C"
