@@ -70,7 +70,14 @@ def parse():
     ap.add_argument("--c5", action="store_true",
                     help="SURVEY 8d C5: log-uniform 512 B-64 KiB records, AEAD + fused HMAC-SHA256, "
                          "host-resident (H2D + kernels + D2H), records per GPU = --records")
-    ap.add_argument("--mode", default="aead", choices=["aead", "xor", "wire", "store"],
+    ap.add_argument("--pow-jobs", type=int, default=65536, help="--mode pow: jobs per GPU")
+    ap.add_argument("--pow-attempts", type=int, default=4096,
+                    help="--mode pow: attempts per job (difficulty 24 = the store clamp, so nearly "
+                         "every job scans all of them)")
+    ap.add_argument("--pow-schedule", type=int, default=1, choices=[0, 1],
+                    help="--mode pow: 1 = store PoW (mt19937_64 candidates, 44-byte prefix), "
+                         "0 = handshake PoW (start + attempt, 88-byte prefix)")
+    ap.add_argument("--mode", default="aead", choices=["aead", "xor", "wire", "store", "pow"],
                     help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline "
                          "probe); wire = session wire frames seal+open (SURVEY 8f row 1, messages "
                          "of --record-bytes); store = chunk store+fetch pipeline (8f row 2)")
@@ -258,8 +265,120 @@ def c5(args) -> dict:
     return res
 
 
+def pow_bench(args) -> dict:
+    """batched proof-of-work search on the device.  --pow-jobs jobs per GPU,
+    each scanning --pow-attempts candidates at difficulty 24 (StoreProof.cpp's clamp: nearly
+    never found, so every job does the full scan), prefixes resident in HBM.  value = candidate
+    SHA-256 evaluations per second over all ranks.  CPU baseline: the oracle's search loop (the
+    reference's algorithm, StoreProof.cpp:123-146 / Node.cpp:269-292) on the host cores."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ephemeralnet_amd as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    n, A, sched = args.pow_jobs, args.pow_attempts, args.pow_schedule
+    plen = 44 if sched == 1 else 88  # store prefix (empty hint) / handshake prefix
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    pre = torch.randint(0, 256, (n * plen,), dtype=torch.uint8, device=dev, generator=g)
+    offs = torch.arange(0, (n + 1) * plen, plen, dtype=torch.int64, device=dev)
+    diff = torch.full((n,), 24, dtype=torch.uint8, device=dev)
+    nonces = torch.empty(n, dtype=torch.int64, device=dev)
+    atts = torch.empty(n, dtype=torch.int64, device=dev)
+    found = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        E.pow_search(pre, offs, diff, sched, A, nonces, found, atts, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    e1.synchronize()
+    launch_ms = e0.elapsed_time(e1) / args.steps
+    # hashes actually evaluated: attempts up to the found one (+1 seed digest per job)
+    at = atts.cpu().numpy()
+    hashed = int(np.minimum(at + 1, A).sum()) + n
+    out = None
+    if rank == 0:
+        value = hashed * args.steps * world / el
+        out = {
+            "metric": "G SHA-256 PoW candidates/s (device-resident batch search)",
+            "value": round(value / 1e9, 3),
+            "unit": "G candidates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "dtype": "u32",
+            "data": "synthetic random prefixes (torch.randint on device)",
+            "config": {"workload": f"{'store' if sched else 'handshake'} PoW: {n} jobs x {A} attempts, "
+                                   f"{plen}-byte prefixes, difficulty 24",
+                       "jobs_per_gpu": n, "attempts": A, "schedule": sched,
+                       "found": int(found.sum().item())},
+            "launch_ms": round(launch_ms, 4),
+            "compressions_per_candidate": 1,
+            "sha_rounds_per_candidate": 64 - plen % 64 // 4,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            import ctypes as C
+
+            import oracle
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+            m = 64 * threads
+            pre_h = np.frombuffer(os.urandom(m * plen), dtype=np.uint8).copy()
+            off_h = np.arange(0, (m + 1) * plen, plen, dtype=np.uint64)
+            cpu_att = max(256, int(args.cpu_seconds * 2e6 / m))  # ~2 M hashes/s per thread budget
+            hh = C.c_uint64()
+            secs = oracle.lib().orc_bench_pow(pre_h.ctypes.data_as(C.c_void_p),
+                                              off_h.ctypes.data_as(C.c_void_p), m, 24, cpu_att,
+                                              threads, C.byref(hh))
+            out["cpu_baseline"] = {
+                "value": round(hh.value / secs / 1e9, 5), "unit": "G candidates/s", "cores": threads,
+                "kind": "port",
+                "sample": f"{m} node-schedule jobs x {cpu_att} attempts, {plen}-byte prefixes "
+                          "(oracle/enet_oracle.c orc_pow_search, byte-wise SHA-256 like "
+                          "src/crypto/Sha256.cpp, -O2)"}
+    if world > 1:
+        dist.destroy_process_group()
+    return out
+
+
 def main():
     args = parse()
+    if args.mode == "pow":
+        r = pow_bench(args)
+        if r:
+            print(json.dumps(r), flush=True)
+        return
     if args.c5:
         r = c5(args)
         if r:

@@ -3,17 +3,22 @@
 // kernels and copies the result back; there is no CPU crypto path in the product (a failing
 // GPU path throws std::runtime_error instead of silently computing on the host).
 //
-// Reference: src/crypto/{ChaCha20,Sha256,HmacSha256,CryptoManager}.cpp (ShardianLabs/EphemeralNet).
+// Reference: src/crypto/{ChaCha20,Sha256,HmacSha256,CryptoManager}.cpp, src/security/StoreProof.cpp,
+// src/network/KeyManager.cpp and the PoW searches of src/core/Node.cpp (ShardianLabs/EphemeralNet).
 #include "ephemeralnet/crypto/Batch.hpp"
 #include "ephemeralnet/crypto/ChaCha20.hpp"
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 #include "ephemeralnet/crypto/HmacSha256.hpp"
 #include "ephemeralnet/crypto/Sha256.hpp"
+#include "ephemeralnet/network/KeyManager.hpp"
+#include "ephemeralnet/security/StoreProof.hpp"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstring>
+#include <filesystem>
+#include <limits>
 #include <random>
 #include <stdexcept>
 #include <string>
@@ -559,5 +564,289 @@ std::vector<std::vector<std::uint8_t>> FrameQueue::flush() {
     return frames;
 }
 
+// ------------------------------------------------------------------------------ proof of work
+namespace {
+void put_be64(std::vector<std::uint8_t>& v, std::uint64_t x) {
+    for (int i = 0; i < 8; ++i) v.push_back(static_cast<std::uint8_t>(x >> (56 - 8 * i)));
+}
+void put_lp64(std::vector<std::uint8_t>& v, const std::uint8_t* p, std::size_t n) {  // Node.cpp:149-153
+    put_be64(v, n);
+    v.insert(v.end(), p, p + n);
+}
+}  // namespace
+
+std::vector<PowResult> pow_search(std::span<const std::span<const std::uint8_t>> prefixes,
+                                  std::span<const std::uint8_t> difficulty, PowSchedule schedule,
+                                  std::uint64_t max_attempts) {
+    const size_t n = prefixes.size();
+    if (difficulty.size() != n) throw std::invalid_argument("enet batch::pow_search: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(prefixes);
+    auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
+    auto* dd = (uint8_t*)st.get(S_AUX, n);
+    auto* dnonce = (uint64_t*)st.get(S_OUT, 8 * n);
+    auto* datt = (uint64_t*)st.get(S_TAGS, 8 * n);
+    auto* dfound = (uint8_t*)st.get(S_OK, n);
+    st.h2d(din, in.arena.data(), in.arena.size());
+    st.h2d(doff, in.off.data(), 8 * (n + 1));
+    st.h2d(dd, difficulty.data(), n);
+    enet_check(enet_pow_search_batch((uint32_t)n, din, doff, dd, static_cast<int>(schedule), max_attempts,
+                                     dnonce, datt, dfound, st.s()),
+               "pow_search");
+    std::vector<std::uint64_t> nonce(n), att(n);
+    std::vector<std::uint8_t> found(n);
+    st.d2h(nonce.data(), dnonce, 8 * n);
+    st.d2h(att.data(), datt, 8 * n);
+    st.d2h(found.data(), dfound, n);
+    st.sync();
+    std::vector<PowResult> res(n);
+    for (size_t i = 0; i < n; ++i) res[i] = PowResult{found[i] != 0, nonce[i], att[i]};
+    return res;
+}
+
+std::vector<std::uint8_t> pow_check(std::span<const std::span<const std::uint8_t>> prefixes,
+                                    std::span<const std::uint64_t> nonces,
+                                    std::span<const std::uint8_t> difficulty) {
+    const size_t n = prefixes.size();
+    if (difficulty.size() != n || nonces.size() != n)
+        throw std::invalid_argument("enet batch::pow_check: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    Packed in = pack(prefixes);
+    auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
+    auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
+    auto* dd = (uint8_t*)st.get(S_AUX, n);
+    auto* dnonce = (uint64_t*)st.get(S_CTR, 8 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    st.h2d(din, in.arena.data(), in.arena.size());
+    st.h2d(doff, in.off.data(), 8 * (n + 1));
+    st.h2d(dd, difficulty.data(), n);
+    st.h2d(dnonce, nonces.data(), 8 * n);
+    enet_check(enet_pow_check_batch((uint32_t)n, din, doff, dnonce, dd, dok, st.s()), "pow_check");
+    std::vector<std::uint8_t> ok(n);
+    st.d2h(ok.data(), dok, n);
+    st.sync();
+    return ok;
+}
+
+std::vector<std::uint8_t> announce_pow_prefix(const ChunkId& chunk_id, const PeerId& peer_id,
+                                              std::string_view endpoint, std::string_view manifest_uri,
+                                              std::span<const std::uint8_t> assigned_shards,
+                                              std::int64_t ttl_seconds) {
+    std::vector<std::uint8_t> v;
+    v.reserve(120 + endpoint.size() + manifest_uri.size() + assigned_shards.size());
+    put_lp64(v, chunk_id.data(), chunk_id.size());
+    put_lp64(v, peer_id.data(), peer_id.size());
+    put_lp64(v, reinterpret_cast<const std::uint8_t*>(endpoint.data()), endpoint.size());
+    put_lp64(v, reinterpret_cast<const std::uint8_t*>(manifest_uri.data()), manifest_uri.size());
+    put_lp64(v, assigned_shards.data(), assigned_shards.size());
+    put_be64(v, static_cast<std::uint64_t>(ttl_seconds));  // Node.cpp:165-166
+    return v;
+}
+
+std::vector<std::uint8_t> handshake_pow_prefix(const PeerId& initiator, const PeerId& responder,
+                                               std::uint32_t initiator_public) {
+    std::vector<std::uint8_t> v;
+    v.reserve(88);
+    put_lp64(v, initiator.data(), initiator.size());
+    put_lp64(v, responder.data(), responder.size());
+    put_be64(v, static_cast<std::uint64_t>(initiator_public));  // Node.cpp:241-242
+    return v;
+}
+
+std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secrets,
+                                                       std::span<const std::uint64_t> counters,
+                                                       std::span<const std::int64_t> ticks) {
+    const size_t n = secrets.size();
+    if (counters.size() != n || ticks.size() != n)
+        throw std::invalid_argument("enet batch::session_keys: size mismatch");
+    if (n == 0) return {};
+    Staging& st = staging();
+    auto kf = flat_keys(secrets);
+    auto* dk = (uint8_t*)st.get(S_KEYS, 32 * n);
+    auto* dc = (uint64_t*)st.get(S_CTR, 8 * n);
+    auto* dt = (int64_t*)st.get(S_NONCES, 8 * n);
+    auto* dout = (uint8_t*)st.get(S_OUT, 32 * n);
+    st.h2d(dk, kf.data(), 32 * n);
+    st.h2d(dc, counters.data(), 8 * n);
+    st.h2d(dt, ticks.data(), 8 * n);
+    enet_check(enet_session_key_batch((uint32_t)n, dk, dc, dt, dout, st.s()), "session_keys");
+    std::vector<std::array<std::uint8_t, 32>> res(n);
+    st.d2h(res.data(), dout, 32 * n);
+    st.sync();
+    return res;
+}
+
 }  // namespace batch
 }  // namespace ephemeralnet::crypto
+
+// ------------------------------------------------------------------------------ security::StoreProof
+namespace ephemeralnet::security {
+
+ChunkId derive_chunk_id(std::span<const std::uint8_t> data) { return one_sha(data); }
+
+std::optional<std::string> sanitize_filename_hint(std::string_view raw_path) {
+    if (raw_path.empty()) return std::nullopt;
+    const std::filesystem::path provided(raw_path);
+    const auto base = provided.filename().string();
+    if (base.empty() || base == "." || base == "..") return std::nullopt;
+    constexpr std::size_t kMaxFilenameLength = 255;  // StoreProof.cpp:100
+    if (base.size() <= kMaxFilenameLength) return base;
+    return base.substr(0, kMaxFilenameLength);
+}
+
+std::vector<std::uint8_t> store_pow_prefix(const StoreWorkInput& input) {
+    std::vector<std::uint8_t> v(input.chunk_id.begin(), input.chunk_id.end());
+    for (int i = 0; i < 8; ++i) v.push_back(static_cast<std::uint8_t>(input.payload_size >> (56 - 8 * i)));
+    const auto len = static_cast<std::uint32_t>(
+        std::min<std::size_t>(input.filename_hint.size(), std::numeric_limits<std::uint32_t>::max()));
+    for (int i = 0; i < 4; ++i) v.push_back(static_cast<std::uint8_t>(len >> (24 - 8 * i)));
+    v.insert(v.end(), input.filename_hint.begin(), input.filename_hint.end());
+    return v;
+}
+
+namespace {
+std::uint8_t clamp_store_difficulty(std::uint8_t d) {  // StoreProof.cpp:114-116, 128-130
+    return d > kMaxStorePowDifficulty ? kMaxStorePowDifficulty : d;
+}
+}  // namespace
+
+namespace batch {
+std::vector<std::optional<std::uint64_t>> compute_store_pow(std::span<const StoreWorkInput> inputs,
+                                                            std::uint8_t difficulty_bits,
+                                                            std::uint64_t max_attempts) {
+    std::vector<std::optional<std::uint64_t>> res(inputs.size());
+    if (inputs.empty()) return res;
+    if (difficulty_bits == 0) {  // StoreProof.cpp:125-127
+        for (auto& r : res) r = std::uint64_t{0};
+        return res;
+    }
+    const std::uint8_t d = clamp_store_difficulty(difficulty_bits);
+    if (max_attempts == 0) max_attempts = kDefaultStorePowMaxAttempts;  // :131-133
+    std::vector<std::vector<std::uint8_t>> pre;
+    pre.reserve(inputs.size());
+    for (const auto& in : inputs) pre.push_back(store_pow_prefix(in));
+    std::vector<std::span<const std::uint8_t>> views(pre.begin(), pre.end());
+    std::vector<std::uint8_t> diffs(inputs.size(), d);
+    auto r = crypto::batch::pow_search(views, diffs, crypto::batch::PowSchedule::Store, max_attempts);
+    for (size_t i = 0; i < r.size(); ++i)
+        if (r[i].found) res[i] = r[i].nonce;
+    return res;
+}
+
+std::vector<std::uint8_t> store_pow_valid(std::span<const StoreWorkInput> inputs,
+                                          std::span<const std::uint64_t> nonces,
+                                          std::uint8_t difficulty_bits) {
+    if (nonces.size() != inputs.size()) throw std::invalid_argument("enet store_pow_valid: size mismatch");
+    if (difficulty_bits == 0) return std::vector<std::uint8_t>(inputs.size(), 1);  // :112-113
+    std::vector<std::vector<std::uint8_t>> pre;
+    pre.reserve(inputs.size());
+    for (const auto& in : inputs) pre.push_back(store_pow_prefix(in));
+    std::vector<std::span<const std::uint8_t>> views(pre.begin(), pre.end());
+    std::vector<std::uint8_t> diffs(inputs.size(), clamp_store_difficulty(difficulty_bits));
+    return crypto::batch::pow_check(views, nonces, diffs);
+}
+}  // namespace batch
+
+bool store_pow_valid(const StoreWorkInput& input, std::uint64_t nonce, std::uint8_t difficulty_bits) {
+    return batch::store_pow_valid(std::span(&input, 1), std::span(&nonce, 1), difficulty_bits)[0] == 1;
+}
+
+std::optional<std::uint64_t> compute_store_pow(const StoreWorkInput& input, std::uint8_t difficulty_bits,
+                                               std::uint64_t max_attempts) {
+    return batch::compute_store_pow(std::span(&input, 1), difficulty_bits, max_attempts)[0];
+}
+
+}  // namespace ephemeralnet::security
+
+// ------------------------------------------------------------------------------ network::KeyManager
+namespace ephemeralnet::network {
+
+namespace {
+std::int64_t ticks_of(std::chrono::steady_clock::time_point t) {  // KeyManager.cpp:24, 83
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count();
+}
+}  // namespace
+
+KeyManager::KeyManager(std::chrono::seconds rotation_interval) : rotation_interval_(rotation_interval) {}
+
+void KeyManager::register_session(const PeerId& peer_id, const crypto::Key& shared_secret) {
+    const auto now = std::chrono::steady_clock::now();
+    std::array<std::uint8_t, 16> material{};  // BE64(counter 0) || BE64(ticks), KeyManager.cpp:15-30
+    const std::uint64_t ticks = static_cast<std::uint64_t>(ticks_of(now));
+    for (int i = 0; i < 8; ++i) material[8 + i] = static_cast<std::uint8_t>(ticks >> (56 - 8 * i));
+    register_session_with_material(peer_id, shared_secret, material, now);
+}
+
+void KeyManager::register_session_with_material(const PeerId& peer_id, const crypto::Key& shared_secret,
+                                                std::span<const std::uint8_t> material,
+                                                std::chrono::steady_clock::time_point reference_time) {
+    SessionKeyContext context{};
+    context.shared_secret = shared_secret;
+    context.last_rotation = reference_time;
+    context.counter = 0;
+    context.current_key = crypto::HmacSha256::compute(shared_secret.bytes, material);  // :42-43
+    contexts_[peer_id] = context;
+}
+
+std::optional<std::array<std::uint8_t, 32>> KeyManager::current_key(const PeerId& peer_id) const {
+    const auto it = contexts_.find(peer_id);
+    if (it == contexts_.end()) return std::nullopt;
+    return it->second.current_key;
+}
+
+std::optional<std::array<std::uint8_t, 32>> KeyManager::rotate_if_needed(
+    const PeerId& peer_id, std::chrono::steady_clock::time_point now) {
+    auto it = contexts_.find(peer_id);
+    if (it == contexts_.end()) return std::nullopt;
+    auto& context = it->second;
+    if (now - context.last_rotation < rotation_interval_) return std::nullopt;  // :63-65
+    context.counter += 1;
+    context.last_rotation = now;
+    const std::uint64_t ctr[1] = {context.counter};
+    const std::int64_t tk[1] = {ticks_of(now)};
+    context.current_key = crypto::batch::session_keys(std::span(&context.shared_secret, 1), ctr, tk)[0];
+    return context.current_key;
+}
+
+std::vector<PeerId> KeyManager::known_peers() const {
+    std::vector<PeerId> peers;
+    peers.reserve(contexts_.size());
+    for (const auto& [peer, context] : contexts_) {
+        (void)context;
+        peers.push_back(peer);
+    }
+    return peers;
+}
+
+std::vector<std::pair<PeerId, std::array<std::uint8_t, 32>>> KeyManager::rotate_all_due(
+    std::chrono::steady_clock::time_point now) {
+    std::vector<SessionKeyContext*> due;
+    std::vector<PeerId> peers;
+    std::vector<crypto::Key> secrets;
+    std::vector<std::uint64_t> counters;
+    std::vector<std::int64_t> ticks;
+    for (auto& [peer, context] : contexts_) {
+        if (now - context.last_rotation < rotation_interval_) continue;
+        due.push_back(&context);
+        peers.push_back(peer);
+        secrets.push_back(context.shared_secret);
+        counters.push_back(context.counter + 1);
+        ticks.push_back(ticks_of(now));
+    }
+    std::vector<std::pair<PeerId, std::array<std::uint8_t, 32>>> out;
+    if (due.empty()) return out;
+    auto keys = crypto::batch::session_keys(secrets, counters, ticks);
+    out.reserve(due.size());
+    for (size_t i = 0; i < due.size(); ++i) {
+        due[i]->counter = counters[i];
+        due[i]->last_rotation = now;
+        due[i]->current_key = keys[i];
+        out.emplace_back(peers[i], keys[i]);
+    }
+    return out;
+}
+
+}  // namespace ephemeralnet::network

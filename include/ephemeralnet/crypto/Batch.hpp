@@ -7,6 +7,7 @@
 #include <array>
 #include <cstdint>
 #include <span>
+#include <string_view>
 #include <vector>
 
 #include "ephemeralnet/Types.hpp"
@@ -93,5 +94,41 @@ private:
     std::vector<Nonce> nonces_;
     std::vector<std::vector<std::uint8_t>> messages_;
 };
+
+// Proof of work.  Every PoW in the reference hashes
+// SHA-256(prefix || BE64(nonce)) and takes the first nonce, in attempt order, with >= difficulty
+// leading zero bits.  Node: compute_announce_pow / compute_handshake_pow (Node.cpp:212-230,
+// 269-292; candidates start + attempt).  Store: security::compute_store_pow (StoreProof.cpp;
+// successive mt19937_64 outputs) -- see also ephemeralnet/security/StoreProof.hpp.
+enum class PowSchedule : int { Node = 0, Store = 1 };
+struct PowResult {
+    bool found{false};
+    std::uint64_t nonce{0};
+    std::uint64_t attempts{0};  // index of the nonce in attempt order (max_attempts if not found)
+};
+// difficulty[i] as given (no clamp; 0 -> nonce 0); one device pass for the whole batch
+ENET_CXX_API std::vector<PowResult> pow_search(std::span<const std::span<const std::uint8_t>> prefixes,
+                                               std::span<const std::uint8_t> difficulty,
+                                               PowSchedule schedule, std::uint64_t max_attempts);
+// announce_pow_valid / handshake_pow_valid / store_pow_valid without the clamp; 1 = valid
+ENET_CXX_API std::vector<std::uint8_t> pow_check(std::span<const std::span<const std::uint8_t>> prefixes,
+                                                 std::span<const std::uint64_t> nonces,
+                                                 std::span<const std::uint8_t> difficulty);
+// Node.cpp:155-171 (announce_pow_digest without the nonce): BE64-length-prefixed chunk_id,
+// peer_id, endpoint, manifest_uri, assigned_shards, then BE64(ttl seconds)
+ENET_CXX_API std::vector<std::uint8_t> announce_pow_prefix(const ChunkId& chunk_id, const PeerId& peer_id,
+                                                           std::string_view endpoint,
+                                                           std::string_view manifest_uri,
+                                                           std::span<const std::uint8_t> assigned_shards,
+                                                           std::int64_t ttl_seconds);
+// Node.cpp:233-245 (handshake_pow_digest without the nonce)
+ENET_CXX_API std::vector<std::uint8_t> handshake_pow_prefix(const PeerId& initiator, const PeerId& responder,
+                                                            std::uint32_t initiator_public);
+
+// KeyManager::derive_key (KeyManager.cpp:74-92) for many sessions:
+// HMAC-SHA256(secret_i, BE64(counter_i) || BE64(ticks_i)), ticks in ns since the steady_clock epoch
+ENET_CXX_API std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secrets,
+                                                                    std::span<const std::uint64_t> counters,
+                                                                    std::span<const std::int64_t> ticks);
 
 }  // namespace ephemeralnet::crypto::batch

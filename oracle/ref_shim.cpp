@@ -142,6 +142,14 @@ int ref_store_pow_valid(const uint8_t* chunk_id, uint64_t payload_size, const ch
     return security::store_pow_valid(in, nonce, difficulty) ? 1 : 0;
 }
 
+// security::sanitize_filename_hint (StoreProof.cpp:91-107): length, or -1 for nullopt
+long ref_sanitize_filename_hint(const char* p, size_t n, char* out, size_t cap) {
+    auto r = security::sanitize_filename_hint(std::string_view(p, n));
+    if (!r) return -1;
+    if (r->size() <= cap) std::memcpy(out, r->data(), r->size());
+    return (long)r->size();
+}
+
 // std::mt19937_64 and the full-range uniform_int_distribution draw Node.cpp:217-220 / 279-282 use
 void ref_mt64(uint64_t seed, size_t n, uint64_t* out) {
     std::mt19937_64 g(seed);

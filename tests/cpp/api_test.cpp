@@ -1,6 +1,7 @@
 // api_test.cpp -- exercises the reference C++ API (ephemeralnet::crypto, same signatures as the
 // reference headers) exactly as a reference caller would, against libenet_crypto.so.
 // Reads one operation per line on stdin, prints one hex result per line.
+#include <chrono>
 #include <cstdio>
 #include <iostream>
 #include <sstream>
@@ -12,6 +13,8 @@
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 #include "ephemeralnet/crypto/HmacSha256.hpp"
 #include "ephemeralnet/crypto/Sha256.hpp"
+#include "ephemeralnet/network/KeyManager.hpp"
+#include "ephemeralnet/security/StoreProof.hpp"
 #include "enet_crypto.h"
 
 using namespace ephemeralnet;
@@ -146,6 +149,81 @@ int main() {
             std::span<const uint8_t> ps[1] = {pb};
             auto s = crypto::batch::aead_seal(std::span(&key, 1), std::span(&nonce, 1), ps);
             std::cout << hex(s[0].data) << " " << hex(s[0].tag) << "\n";
+        } else if (op == "store_pow") {
+            // security::compute_store_pow / store_pow_valid (reference StoreProof.hpp signatures)
+            std::string id, size, hint, d, mx; in >> id >> size >> hint >> d >> mx;
+            auto ib = unhex(id), hb = unhex(hint);
+            std::string hs(hb.begin(), hb.end());
+            security::StoreWorkInput w{};
+            std::copy(ib.begin(), ib.end(), w.chunk_id.begin());
+            w.payload_size = std::stoull(size);
+            w.filename_hint = hs;
+            const auto diff = (uint8_t)std::stoul(d);
+            auto r = security::compute_store_pow(w, diff, std::stoull(mx));
+            if (!r) {
+                std::cout << "none\n";
+            } else {
+                std::cout << *r << " " << (security::store_pow_valid(w, *r, diff) ? 1 : 0) << " "
+                          << (security::store_pow_valid(w, *r + 1, diff) ? 1 : 0) << "\n";
+            }
+        } else if (op == "handshake_pow") {
+            std::string a, b, pub, d; in >> a >> b >> pub >> d;
+            PeerId ia{}, ib{};
+            auto ab = unhex(a), bb = unhex(b);
+            std::copy(ab.begin(), ab.end(), ia.begin());
+            std::copy(bb.begin(), bb.end(), ib.begin());
+            auto pre = crypto::batch::handshake_pow_prefix(ia, ib, (uint32_t)std::stoul(pub));
+            std::span<const uint8_t> ps[1] = {pre};
+            const uint8_t diff[1] = {(uint8_t)std::stoul(d)};
+            auto r = crypto::batch::pow_search(ps, diff, crypto::batch::PowSchedule::Node, 500000);
+            const uint64_t nn[1] = {r[0].nonce};
+            auto ok = crypto::batch::pow_check(ps, nn, diff);
+            std::cout << (r[0].found ? 1 : 0) << " " << r[0].nonce << " " << r[0].attempts << " "
+                      << (int)ok[0] << "\n";
+        } else if (op == "announce_pow") {
+            std::string id, peer, ep, uri, sh, ttl, d; in >> id >> peer >> ep >> uri >> sh >> ttl >> d;
+            ChunkId cid{}; PeerId pid{};
+            auto ib = unhex(id), pb = unhex(peer), eb = unhex(ep), ub = unhex(uri), sb = unhex(sh);
+            std::copy(ib.begin(), ib.end(), cid.begin());
+            std::copy(pb.begin(), pb.end(), pid.begin());
+            auto pre = crypto::batch::announce_pow_prefix(cid, pid, std::string(eb.begin(), eb.end()),
+                                                          std::string(ub.begin(), ub.end()), sb,
+                                                          std::stoll(ttl));
+            std::span<const uint8_t> ps[1] = {pre};
+            const uint8_t diff[1] = {(uint8_t)std::stoul(d)};
+            auto r = crypto::batch::pow_search(ps, diff, crypto::batch::PowSchedule::Node, 500000);
+            std::cout << (r[0].found ? 1 : 0) << " " << r[0].nonce << " " << r[0].attempts << "\n";
+        } else if (op == "keymgr") {
+            // KeyManager: register_session_with_material, then rotate_if_needed / rotate_all_due
+            std::string sec, mat, ticks; in >> sec >> mat >> ticks;
+            crypto::Key k{};
+            auto kb = unhex(sec);
+            std::copy(kb.begin(), kb.end(), k.bytes.begin());
+            auto mb = unhex(mat);
+            const auto t0 = std::chrono::steady_clock::time_point{};
+            const auto now = t0 + std::chrono::nanoseconds(std::stoll(ticks));
+            network::KeyManager km(std::chrono::seconds(1));
+            PeerId p1{}, p2{}, p3{};
+            p1[0] = 1; p2[0] = 2; p3[0] = 3;
+            km.register_session_with_material(p1, k, mb, t0);
+            km.register_session_with_material(p2, k, mb, t0);
+            km.register_session_with_material(p3, k, mb, now);  // not due at `now`
+            const auto mk = *km.current_key(p1);
+            const bool early = !km.rotate_if_needed(p1, t0 + std::chrono::milliseconds(500));
+            const auto rk = km.rotate_if_needed(p1, now);
+            auto all = km.rotate_all_due(now);  // p2 only (p1 was just rotated)
+            const bool batch_ok = all.size() == 1 && all[0].first == p2 && rk && all[0].second == *rk &&
+                                  *km.current_key(p3) == mk && km.known_peers().size() == 3 && early;
+            std::cout << hex(mk) << " " << (rk ? hex(*rk) : std::string("-")) << " " << (batch_ok ? 1 : 0)
+                      << "\n";
+        } else if (op == "sanitize") {
+            std::string raw; in >> raw;
+            auto rb = unhex(raw);
+            auto r = security::sanitize_filename_hint(std::string(rb.begin(), rb.end()));
+            std::cout << (r ? hex(*r) : std::string("none")) << "\n";
+        } else if (op == "chunk_id") {
+            std::string d; in >> d;
+            std::cout << hex(security::derive_chunk_id(unhex(d))) << "\n";
         } else if (!op.empty()) {
             std::cout << "?\n";
         }

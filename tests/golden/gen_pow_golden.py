@@ -38,6 +38,8 @@ REF.ref_sha256_concat.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p
 REF.ref_keymanager_material_key.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t, C.c_void_p]
 REF.ref_keymanager_rotate.argtypes = [C.c_char_p, C.c_int64, C.c_void_p]
 REF.ref_keymanager_rotate.restype = C.c_int64
+REF.ref_sanitize_filename_hint.argtypes = [C.c_char_p, C.c_size_t, C.c_void_p, C.c_size_t]
+REF.ref_sanitize_filename_hint.restype = C.c_long
 
 
 def be64(v: int) -> bytes:
@@ -168,6 +170,15 @@ def main():
         ks.append({"secret": secret.hex(), "material": material.hex(), "material_key": bytes(o).hex(),
                    "rotate_ticks": now, "rotate_counter": 1, "rotated_key": bytes(o2).hex()})
     g["session_keys"] = ks
+
+    # -- sanitize_filename_hint (StoreProof.cpp:91-107)
+    sn = []
+    for raw in [b"", b".", b"..", b"a.txt", b"/tmp/x/report.pdf", b"dir/", b"C:/data/f.bin", b"./..",
+                b"/abs/" + b"n" * 300, b"rel/path/with space.txt", b"/", b"x/.", b"x/.."]:
+        out = (C.c_char * 512)()
+        n = REF.ref_sanitize_filename_hint(raw, len(raw), out, 512)
+        sn.append({"raw": raw.hex(), "result": None if n < 0 else bytes(out)[:n].hex()})
+    g["sanitize_filename_hint"] = sn
 
     path = os.path.join(HERE, "pow.json")
     with open(path, "w") as f:

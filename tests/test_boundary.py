@@ -61,6 +61,16 @@ def test_cpp_api_exports_reference_signatures(built):
         "ephemeralnet::crypto::CryptoManager::encrypt_with_key(",
         "ephemeralnet::crypto::CryptoManager::decrypt_with_key(",
         "ephemeralnet::crypto::CryptoManager::generate_key()",
+        "ephemeralnet::security::compute_store_pow(ephemeralnet::security::StoreWorkInput const&, "
+        "unsigned char, unsigned long)",
+        "ephemeralnet::security::store_pow_valid(ephemeralnet::security::StoreWorkInput const&, "
+        "unsigned long, unsigned char)",
+        "ephemeralnet::security::derive_chunk_id(std::span<unsigned char const",
+        "ephemeralnet::security::sanitize_filename_hint",
+        "ephemeralnet::network::KeyManager::rotate_if_needed(",
+        "ephemeralnet::network::KeyManager::register_session_with_material(",
+        "ephemeralnet::network::KeyManager::current_key(",
+        "ephemeralnet::crypto::batch::pow_search(",
     ]:
         assert sig in out, sig
 
@@ -99,6 +109,14 @@ def test_invalid_arguments_rejected_without_gpu(built):
     assert L.enet_chacha20_xor_batch(None, None, None) == -1
     r.count = 0  # empty batch is a no-op
     assert L.enet_chacha20_xor_batch(C.byref(r), None, None) == 0
+    # proof of work / session keys: NULL buffers and unknown schedules are rejected on the host
+    assert L.enet_pow_search_batch(3, None, None, None, 0, 10, None, None, None, None) == -1
+    buf = (C.c_uint8 * 64)()
+    assert L.enet_pow_search_batch(3, buf, buf, buf, 7, 10, buf, None, buf, None) == -1
+    assert b"schedule" in L.enet_last_error()
+    assert L.enet_pow_check_batch(3, buf, None, buf, buf, buf, None) == -1
+    assert L.enet_session_key_batch(3, None, buf, buf, buf, None) == -1
+    assert L.enet_pow_search_batch(0, None, None, None, 0, 10, None, None, None, None) == 0
 
 
 def test_product_never_imports_oracle():

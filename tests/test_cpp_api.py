@@ -104,3 +104,42 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
             assert body == oracle.frame_seal(key, nonce, m)
         else:
             assert got == e, op[:60]
+
+
+@pytest.mark.gpu
+def test_cpp_pow_and_keys_match_reference_golden(api_bin):
+    """security::StoreProof, crypto::batch PoW (Node.cpp announce / handshake) and
+    network::KeyManager through the reference C++ signatures against tests/golden/pow.json."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "pow.json")) as f:
+        pg = json.load(f)
+    ops, expect = [], []
+    for c in pg["store_pow"]:
+        if c["max_attempts"] == 0:
+            continue
+        ops.append(f"store_pow {c['chunk_id']} {c['payload_size']} {c['hint'] or '-'} {c['difficulty']} "
+                   f"{c['max_attempts']}")
+        expect.append(f"{c['nonce']} {int(c['valid'])} {int(c['valid_next'])}" if c["found"] else "none")
+    for c in pg["handshake_pow"]:
+        ops.append(f"handshake_pow {c['initiator']} {c['responder']} {c['public']} {c['difficulty']}")
+        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} 1")
+    for c in pg["announce_pow"]:
+        ops.append("announce_pow " + " ".join(c[k] or "-" for k in ("chunk_id", "peer_id", "endpoint",
+                                                                   "manifest_uri", "assigned_shards"))
+                   + f" {c['ttl']} {c['difficulty']}")
+        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']}")
+    for c in pg["session_keys"]:
+        ops.append(f"keymgr {c['secret']} {c['material']} {c['rotate_ticks']}")
+        expect.append(f"{c['material_key']} {c['rotated_key']} 1")
+    for c in pg["sanitize_filename_hint"]:
+        ops.append(f"sanitize {c['raw'] or '-'}")
+        expect.append(c["result"] if c["result"] is not None else "none")
+    for L in (0, 1, 4096):
+        d = splitmix_bytes(40000 + L, L)
+        ops.append(f"chunk_id {h(d)}")
+        expect.append(hashlib.sha256(d).hexdigest())
+    res = subprocess.run([api_bin], input="\n".join(ops) + "\n", capture_output=True, text=True,
+                         check=True, timeout=300).stdout.splitlines()
+    assert len(res) == len(ops)
+    for op, e, got in zip(ops, expect, res):
+        assert got == e, op[:80]
