@@ -205,7 +205,8 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
     if (COOP == 0) poly_setup();
 
     // ---- cooperative stages (uniform batches)
-    uint32_t cco = cbeg;  // first block left for the per-lane paths
+    uint32_t cco = cbeg;     // first block left for the per-lane fast path
+    uint32_t ctail = cfast;  // first block left for the per-lane tail path
     if (COOP == 1) {
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t wbase = threadIdx.x & ~63u;
@@ -304,6 +305,118 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             land();
         }
         cco = min(cfast, cbeg + kStage * Ts);
+        // Ragged last stage (one lane per record): bytes [kRun*Ts, L) of every record -- the odd
+        // whole block and the partial block -- through the same whole-line LDS transposition
+        // instead of the per-lane paths (64 scattered records per load/store instruction).
+        // rem = L - kRun*Ts is uniform; chunks [0, rem/16) move whole, and a partial chunk is
+        // replaced by the 16-byte window ending at the record end (inside the record since
+        // rem >= 16): loaded there and stored there, so nothing outside the record is read or
+        // written (the window's overlap with the previous chunk is rewritten with equal bytes).
+        const uint32_t rem = (uint32_t)(Lu - (uint64_t)kRun * Ts);
+        if (P == 1 && Lu <= 0xFFFFFFFFull && rem >= 16u) {
+            const uint32_t rem16 = rem >> 4, remb = rem & 15u;
+            const uint32_t nch = rem16 + (remb ? 1u : 0u);
+            const uint64_t adv = (uint64_t)kRun * Ts;
+            // (a) loads: lane (owner 8i + lane/8, LDS slot kk) fetches the record chunk kk ^ sw
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t o = 8u * i + (lane >> 3);
+                const uint32_t gc = kk ^ ((o >> 1) & 7u);
+                const uint64_t run = (uint64_t)((wgid0 + o) >> LOGP) * Lu + adv;
+                if (gc < nch) {
+                    const uint32_t at = gc < rem16 ? 16u * gc : rem - 16u;
+                    const uint4 v = *reinterpret_cast<const uint4*>(ibase + run + at);
+                    *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) = v;
+                }
+            }
+            ENET_WAVE_LDS_SYNC();
+            // (b) own run -> 32 words, zero past rem (the window slot is shifted into place)
+            uint32_t x[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                uint32_t v4[4] = {0u, 0u, 0u, 0u};
+                if ((uint32_t)k < nch) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                    v4[0] = v.x; v4[1] = v.y; v4[2] = v.z; v4[3] = v.w;
+                    if ((uint32_t)k == rem16) {  // window bytes [rem-16, rem) -> [16k, rem)
+                        uint32_t sh[4];
+                        extract_bytes<4, 4>(v4, 16u - remb, sh);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) v4[t] = sh[t];
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) x[4 * k + t] = v4[t];
+            }
+            // (c) keystream, Poly1305 over the ciphertext chunks [0, nch)
+            const uint32_t c0 = ctr0 + cbeg + kStage * Ts;
+            if (MODE == MODE_OPEN) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if ((uint32_t)u < nch)
+                        poly32_block(h, PR, x[4 * u], x[4 * u + 1], x[4 * u + 2], x[4 * u + 3], 1u);
+            }
+            {
+                uint32_t ks[16];
+                chacha_block(R, c0, ks);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] ^= ks[i];
+            }
+            if (rem > 64u) {
+                uint32_t ks[16];
+                chacha_block(R, c0 + 1, ks);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[16 + i] ^= ks[i];
+            }
+            if (MODE == MODE_SEAL) {
+                // ciphertext bytes past rem are keystream: RFC 8439 pads the last block with zeros
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint32_t lo = 16u * k;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t b0 = lo + 4u * t;
+                        const uint32_t m = rem >= b0 + 4u ? 0xffffffffu
+                                         : rem <= b0      ? 0u
+                                                          : (1u << (8u * (rem - b0))) - 1u;
+                        if ((uint32_t)k == rem16) x[4 * k + t] &= m;
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if ((uint32_t)u < nch)
+                        poly32_block(h, PR, x[4 * u], x[4 * u + 1], x[4 * u + 2], x[4 * u + 3], 1u);
+            }
+            // (d) outputs into the own run: whole chunks, and the window ending at rem
+            uint32_t win[4] = {0u, 0u, 0u, 0u};
+            if (remb) extract_bytes<32, 4>(x, rem - 16u, win);
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if ((uint32_t)k < rem16)
+                    *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                        make_uint4(x[4 * k], x[4 * k + 1], x[4 * k + 2], x[4 * k + 3]);
+                else if ((uint32_t)k == rem16 && remb)
+                    *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                        make_uint4(win[0], win[1], win[2], win[3]);
+            }
+            ENET_WAVE_LDS_SYNC();
+            // (e) lane-linear stores of whole chunks / the window
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t o = 8u * i + (lane >> 3);
+                const uint32_t gc = kk ^ ((o >> 1) & 7u);
+                const uint64_t run = (uint64_t)((wgid0 + o) >> LOGP) * Lu + adv;
+                if (gc < nch) {
+                    const uint32_t at = gc < rem16 ? 16u * gc : rem - 16u;
+                    const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                    *reinterpret_cast<uint4*>(obase + run + at) = v;
+                }
+            }
+            cco = cend;
+            ctail = cend;
+        }
     }
     if (COOP == 3) {
         // Same whole-line stages and wave-private slab as COOP 1, but the loads go straight to
@@ -422,7 +535,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
 
     // ---- tail: the partial block and (frame open) the blocks that touch the MAC
     uint32_t mac[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // frame open: MAC bytes this lane decrypted
-    for (uint32_t c = cfast; c < cend; ++c) {
+    for (uint32_t c = ctail; c < cend; ++c) {
         const uint64_t pos = 64ull * c;
         const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
         if (FRAME == FR_SEAL && pos + 64 > Lin) {

@@ -480,11 +480,16 @@ def test_wire_frames_random_vs_oracle(enet, lanes):
 @pytest.mark.parametrize("staging", [1, 3, 0])
 @pytest.mark.parametrize("L,n,lanes", [(1500, 1000, 1), (1500, 517, 2), (4096, 300, 2),
                                        (4096, 129, 4), (65536, 40, 8), (65536, 33, 16),
-                                       (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1)])
+                                       (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1),
+                                       (1504, 300, 1), (1472, 300, 1), (1400, 300, 1),
+                                       (200, 300, 1), (100, 260, 1), (80, 300, 1), (31, 300, 1),
+                                       (17, 300, 1), (16, 300, 1), (15, 300, 1), (143, 300, 1)])
 def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes, staging):
     """Uniform-length batches take the cooperative LDS-staged path (whole workgroups; staging
     variant 1 = register prefetch, 3 = LDS DMA) plus the per-lane path for the partial
-    workgroup; 1500-byte records start unaligned and end in a partial block."""
+    workgroup; 1500-byte records start unaligned and end in a partial block.  With one lane per
+    record, staging 1 also moves the ragged end (odd block + partial block, >= 16 bytes)
+    through LDS."""
     import torch
     enet.set_lanes_per_record(lanes)
     enet.set_staging(staging)
@@ -509,6 +514,17 @@ def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes, staging):
     enet.aead_open(b2, back, tags, ok)
     assert int(ok.sum()) == n
     assert torch.equal(back, b.arena)
+    if L and n > 6:  # a tampered record is rejected and zeroed, its neighbours are untouched
+        bad = out.clone()
+        o5 = int(b.offsets[5])
+        bad[o5 + L - 1] ^= 1
+        b3 = enet.Batch(bad, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
+        back.fill_(0xAA)
+        enet.aead_open(b3, back, tags, ok)
+        okh = ok.cpu().tolist()
+        assert okh[5] == 0 and sum(okh) == n - 1
+        bh = records_of(host(back), b.offsets.cpu().tolist())
+        assert bh[5] == bytes(L) and bh[4] == items[4] and bh[6] == items[6]
     # xor mode (reference ChaCha20::apply with per-record counters) on the same shape
     ctr = np.frombuffer(splitmix_bytes(L + n, 4 * n), dtype="<u4").copy()
     xo = out_like(b)
