@@ -68,6 +68,9 @@ enet::RecParams rec_params(const enet_records* r) {
     if (r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint)
         p.uniform_len = r->max_len_hint;
     p.coop = (int)enet::staging_variant();
+    // variant 4 = variant 1 without line-aligned staging of unaligned uniform batches
+    p.coop_lines = p.coop == 1 ? 1 : 0;
+    if (p.coop == 4) p.coop = 1;
     // COOP 3 addresses the arena with 32-bit offsets
     if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
     return p;
@@ -95,7 +98,7 @@ uint32_t staging_variant() {
         return s ? (uint32_t)std::strtoul(s, nullptr, 10) + 1u : 0u;
     }();
     if (uint32_t f = g_staging.load(std::memory_order_relaxed)) return f - 1u;
-    if (env == 1 || env == 2 || env == 4) return env - 1u;
+    if (env == 1 || env == 2 || env == 4 || env == 5) return env - 1u;
     return 1u;
 }
 
@@ -143,8 +146,8 @@ uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t ma
 }
 
 int enet_set_staging(int variant) {
-    if (variant != -1 && variant != 0 && variant != 1 && variant != 3)
-        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1 or 3");
+    if (variant != -1 && variant != 0 && variant != 1 && variant != 3 && variant != 4)
+        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 3 or 4");
     enet::g_staging.store((uint32_t)(variant + 1), std::memory_order_relaxed);
     return ENET_OK;
 }

@@ -37,6 +37,9 @@ struct RecParams {
     // uniform batch: every record is exactly uniform_len bytes in and out (0 = not uniform)
     uint64_t uniform_len;
     int coop;  // uniform-batch staging variant: 0 none, 1 register prefetch, 3 LDS DMA
+    // COOP 1 with one lane per record and L % 128 != 0: stage whole aligned 128-byte lines
+    // (COOP 4; needs 4-byte-aligned record starts and in / out starts equal mod 128)
+    int coop_lines;
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the

@@ -87,12 +87,13 @@ __device__ __forceinline__ void poly_block64(uint32_t h[5], const PolyR32& R, co
 
 constexpr uint32_t kStage = 2;                 // blocks per lane per cooperative stage
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
+constexpr uint32_t kRing = 272;                // COOP 4: two-line ring (256 B) + 16 B pad per owner
 
 template <int LOGP, int MODE, int FRAME, int COOP>
 __device__ __forceinline__ void records_body(const RecParams& p) {
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
-    __shared__ __attribute__((aligned(16))) uint8_t slab[COOP ? kWG * kRun : 16];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[COOP == 4 ? kWG * kRing : COOP ? kWG * kRun : 16];
 
     const uint32_t gid = blockIdx.x * kWG + threadIdx.x;
     const uint32_t group = gid >> LOGP;
@@ -418,6 +419,169 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             ctail = cend;
         }
     }
+    if (COOP == 4) {
+        // Line-aligned staging for uniform batches whose records are not 128-byte aligned
+        // (C3: 1 500-byte records), one lane per record.  Run s of a record = record bytes
+        // [128s, 128s+128) straddles two arena lines (offset d = record start mod 128), so
+        // staging whole runs touches twice the lines and splits 16-byte accesses.  Instead the
+        // wave moves whole ALIGNED 128-byte lines: line t of owner o is arena line
+        // floor(start_o / 128) + t, eight lanes per line, eight owners per instruction; each
+        // owner keeps a two-line ring in LDS (slot t % 2) and reads / writes its run at ring
+        // offset (d + 128s) mod 256 with dword accesses.  Line t is complete once run t is
+        // written back (its first d bytes came from run t-1), and is stored whole -- except a
+        // record's first and last lines, shared with the neighbouring records: only this
+        // record's bytes of them are stored (dword-exact; the host launches this variant only
+        // when record starts are 4-byte aligned and in / out starts agree mod 128).  Loads of
+        // whole lines read at most 127 bytes outside the record, never outside its pages.
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint32_t wbase = threadIdx.x & ~63u;
+        const uint32_t Lu = (uint32_t)p.uniform_len;
+        const uint32_t kk = lane & 7u;
+        const uint32_t wgid0 = blockIdx.x * kWG + wbase;
+        const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
+        uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
+        const uint32_t ib = (uint32_t)reinterpret_cast<uintptr_t>(ibase);
+        const uint32_t ob = (uint32_t)reinterpret_cast<uintptr_t>(obase);
+        const uint32_t S = (Lu + kRun - 1) / kRun;  // stages (the last one may be partial)
+        // in and out must share the line phase and allow dword-exact edge stores (uniform test;
+        // otherwise every record takes the per-lane paths below)
+        if (((ib - ob) & 127u) == 0 && (ib & 3u) == 0) {
+        uint8_t* wslab = slab + (wbase >> 6) * (64u * kRing);
+        uint8_t* myring = wslab + lane * kRing;
+        const uint32_t dme = (ib + (wgid0 + lane) * Lu) & 127u;
+        // 32-bit line offsets from the 128-byte-aligned bases (the host launches this variant only
+        // for arenas < 4 GiB)
+        const uint8_t* ial = ibase - (ib & 127u);
+        uint8_t* oal = obase - (ib & 127u);
+        // load / store roles: instruction i serves owner o = 8i + lane/8, 16-byte chunk kk
+        uint32_t roff[8];  // line 0 of owner o
+        uint32_t rgeo[8];  // d | lines << 8 | end-bytes-in-last-line << 16
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t o = 8u * i + (lane >> 3);
+            const uint32_t g = wgid0 + o;
+            const uint32_t d = (ib + g * Lu) & 127u;
+            roff[i] = g * Lu + (ib & 127u) - d;
+            const uint32_t nl = (d + Lu + 127u) >> 7;
+            const uint32_t e = ((d + Lu - 1u) & 127u) + 1u;
+            rgeo[i] = d | (nl << 8) | (e << 16);
+        }
+        uint32_t pf[32];
+        auto fetch = [&](uint32_t t) {  // line t of every role owner -> pf (only lines it has)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (t < ((rgeo[i] >> 8) & 0xffu)) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ial + (roff[i] + 128u * t + 16u * kk));
+                    pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                }
+            }
+        };
+        auto land = [&](uint32_t t) {  // pf -> ring slot t % 2 of every role owner
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint4*>(wslab + (8u * i + (lane >> 3)) * kRing + 128u * (t & 1u) + 16u * kk) =
+                    make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+        };
+        auto store_inner = [&](uint32_t t) {  // line t, 1 <= t <= S-2: complete in every record
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint4*>(oal + (roff[i] + 128u * t + 16u * kk)) =
+                    *reinterpret_cast<const uint4*>(wslab + (8u * i + (lane >> 3)) * kRing +
+                                                    128u * (t & 1u) + 16u * kk);
+        };
+        auto store_line = [&](uint32_t t) {  // ring slot t % 2 -> line t, this record's bytes only
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t d = rgeo[i] & 0xffu, nl = (rgeo[i] >> 8) & 0xffu, e = rgeo[i] >> 16;
+                if (t >= nl) continue;
+                const uint32_t lo = t == 0 ? d : 0u, hi = t + 1 == nl ? e : 128u;
+                const uint32_t c0 = 16u * kk;
+                if (c0 + 16u <= lo || c0 >= hi) continue;
+                const uint4 v = *reinterpret_cast<const uint4*>(
+                    wslab + (8u * i + (lane >> 3)) * kRing + 128u * (t & 1u) + c0);
+                uint8_t* q = oal + (roff[i] + 128u * t + c0);
+                if (c0 >= lo && c0 + 16u <= hi) {
+                    *reinterpret_cast<uint4*>(q) = v;
+                } else {  // a record-boundary chunk: its dwords in [lo, hi) only
+                    const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        if (c0 + 4u * m >= lo && c0 + 4u * m < hi)
+                            *reinterpret_cast<uint32_t*>(q + 4 * m) = w4[m];
+                }
+            }
+        };
+        // dword m of the run at ring offset o (wraps at 256)
+        auto ring_at = [&](uint32_t o, uint32_t m) -> uint32_t* {
+            return reinterpret_cast<uint32_t*>(myring + ((o + 4u * m) & 255u));
+        };
+        fetch(0);
+        poly_setup();  // the one-time-key block runs while line 0 is in flight
+        land(0);
+        fetch(1);
+        for (uint32_t st = 0; st < S; ++st) {
+            ENET_WAVE_LDS_SYNC();
+            land(st + 1);  // lines the owner does not have are never read back
+            ENET_WAVE_LDS_SYNC();
+            const uint32_t rl = min(kRun, Lu - kRun * st);  // uniform
+            uint32_t x[32];
+            uint32_t ro = dme + 128u * (st & 1u);
+#pragma unroll
+            for (int m = 0; m < 32; ++m) x[m] = (4u * m < rl) ? *ring_at(ro, m) : 0u;
+            fetch(st + 2);
+            asm volatile("" : "+v"(R.k[0]) :: "memory");
+            const uint32_t c0 = ctr0 + kStage * st;
+            const uint32_t nch = (rl + 15u) >> 4;
+            if (rl == kRun) {
+                if (MODE == MODE_OPEN) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
+                uint32_t ka[16], kb[16];
+                chacha_block2(R, c0, c0 + 1, ka, kb);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
+                if (MODE == MODE_SEAL) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
+            } else {
+                if (MODE == MODE_OPEN) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if ((uint32_t)u < nch)
+                            poly32_block(h, PR, x[4 * u], x[4 * u + 1], x[4 * u + 2], x[4 * u + 3], 1u);
+                }
+                {
+                    uint32_t ks[16];
+                    chacha_block(R, c0, ks);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) x[i] ^= ks[i];
+                }
+                if (rl > 64u) {
+                    uint32_t ks[16];
+                    chacha_block(R, c0 + 1, ks);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) x[16 + i] ^= ks[i];
+                }
+                if (MODE == MODE_SEAL) {
+#pragma unroll
+                    for (int m = 0; m < 32; ++m) x[m] = (4u * m < rl) ? x[m] : 0u;  // RFC 8439 zero pad
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if ((uint32_t)u < nch)
+                            poly32_block(h, PR, x[4 * u], x[4 * u + 1], x[4 * u + 2], x[4 * u + 3], 1u);
+                }
+            }
+            // recompute the ring addresses here instead of holding 32 of them across the rounds
+            asm volatile("" : "+v"(ro));
+#pragma unroll
+            for (int m = 0; m < 32; ++m)
+                if (4u * m < rl) *ring_at(ro, m) = x[m];
+            ENET_WAVE_LDS_SYNC();
+            if (st >= 1 && st + 2 <= S) store_inner(st);
+            else store_line(st);
+        }
+        ENET_WAVE_LDS_SYNC();
+        store_line(S);  // the last line when the record ends in line S (d + L > 128 S)
+        cco = cend;
+        ctail = cend;
+        }
+    }
     if (COOP == 3) {
         // Same whole-line stages and wave-private slab as COOP 1, but the loads go straight to
         // LDS (global_load_lds_dwordx4: lane-linear destination, the chunk swizzle rides on the
@@ -707,7 +871,13 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            if (p.coop == 3)
+            // (line staging pays its dword realignment only when records are not 16-byte aligned;
+            // 16-byte-aligned runs straddling lines stay faster on the plain run staging)
+            if (LOGP == 0 && p.coop == 1 && (p.uniform_len & 15u) != 0 && (p.uniform_len & 3u) == 0 &&
+                p.uniform_len < (1u << 24) && p.coop_lines &&
+                p.uniform_len * (uint64_t)p.n < 0xFFFFFF00ull)
+                hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 4>), dim3(full), dim3(kWG), 0, s, q);
+            else if (p.coop == 3)
                 hipLaunchKernelGGL((records_kernel_w4<LOGP, MODE>), dim3(full), dim3(kWG), 0, s, q);
             else
                 hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG),

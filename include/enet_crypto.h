@@ -226,8 +226,10 @@ ENET_API uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, ui
  * scheduler.  Returns ENET_EINVAL for other values.  Tuning / test knob. */
 ENET_API int enet_set_lanes_per_record(uint32_t lanes);
 /* Staging of uniform-length batches (all records the same length): 1 = register prefetch + LDS
- * transposition (default), 3 = LDS DMA with one live keystream block (four waves per SIMD),
- * 0 = per-lane path only, -1 restores the default.  Results are identical; tuning / test knob. */
+ * transposition (default; records that are not 128-byte aligned and get one lane each are staged
+ * as whole aligned 128-byte lines), 4 = 1 without the line staging, 3 = LDS DMA with one live
+ * keystream block (four waves per SIMD), 0 = per-lane path only, -1 restores the default.
+ * Results are identical; tuning / test knob. */
 ENET_API int enet_set_staging(int variant);
 /* Human-readable text of the last error on this host thread ("" if none). */
 ENET_API const char* enet_last_error(void);

@@ -95,6 +95,7 @@ def test_library_loads_and_host_helpers(built):
     with pytest.raises(E.EnetError):
         E.set_staging(2)
     E.set_staging(3)
+    E.set_staging(4)
     E.set_staging(-1)
 
 

@@ -477,7 +477,7 @@ def test_wire_frames_random_vs_oracle(enet, lanes):
 
 
 # ------------------------------------------------------------------------------ uniform (COOP)
-@pytest.mark.parametrize("staging", [1, 3, 0])
+@pytest.mark.parametrize("staging", [1, 3, 0, 4])
 @pytest.mark.parametrize("L,n,lanes", [(1500, 1000, 1), (1500, 517, 2), (4096, 300, 2),
                                        (4096, 129, 4), (65536, 40, 8), (65536, 33, 16),
                                        (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1),
@@ -508,6 +508,12 @@ def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes, staging):
         ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
         assert got[i] == ct, (i, L)
         assert th[16 * i:16 * i + 16] == tag, (i, L)
+    # in place (out == in) gives the same ciphertext and tags
+    inp = b.arena.clone()
+    tags_ip = torch.zeros_like(tags)
+    bi = enet.Batch(inp, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    enet.aead_seal(bi, inp, tags_ip)
+    assert torch.equal(inp, out) and torch.equal(tags_ip, tags)
     b2 = enet.Batch(out, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
     back = torch.zeros_like(out)
     ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
