@@ -526,8 +526,13 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             const uint32_t rl = min(kRun, Lu - kRun * st);  // uniform
             uint32_t x[32];
             uint32_t ro = dme + 128u * (st & 1u);
+            if (rl == kRun) {
 #pragma unroll
-            for (int m = 0; m < 32; ++m) x[m] = (4u * m < rl) ? *ring_at(ro, m) : 0u;
+                for (int m = 0; m < 32; ++m) x[m] = *ring_at(ro, m);
+            } else {
+#pragma unroll
+                for (int m = 0; m < 32; ++m) x[m] = (4u * m < rl) ? *ring_at(ro, m) : 0u;
+            }
             fetch(st + 2);
             asm volatile("" : "+v"(R.k[0]) :: "memory");
             const uint32_t c0 = ctr0 + kStage * st;
@@ -569,9 +574,14 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             }
             // recompute the ring addresses here instead of holding 32 of them across the rounds
             asm volatile("" : "+v"(ro));
+            if (rl == kRun) {
 #pragma unroll
-            for (int m = 0; m < 32; ++m)
-                if (4u * m < rl) *ring_at(ro, m) = x[m];
+                for (int m = 0; m < 32; ++m) *ring_at(ro, m) = x[m];
+            } else {
+#pragma unroll
+                for (int m = 0; m < 32; ++m)
+                    if (4u * m < rl) *ring_at(ro, m) = x[m];
+            }
             ENET_WAVE_LDS_SYNC();
             if (st >= 1 && st + 2 <= S) store_inner(st);
             else store_line(st);
@@ -871,9 +881,10 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            // (line staging pays its dword realignment only when records are not 16-byte aligned;
-            // 16-byte-aligned runs straddling lines stay faster on the plain run staging)
-            if (LOGP == 0 && p.coop == 1 && (p.uniform_len & 15u) != 0 && (p.uniform_len & 3u) == 0 &&
+            // (line staging wins whenever records are not 64-byte multiples: 1 M records, 1 GPU,
+            // GiB/s line vs run staging -- 1500 B 746 vs 590, 1504 B 762 vs 689, 1400 B 750 vs
+            // 613; 1472 B 775 vs 789, 1536 B 835 vs 839: tools/c3ab.sh)
+            if (LOGP == 0 && p.coop == 1 && (p.uniform_len & 63u) != 0 && (p.uniform_len & 3u) == 0 &&
                 p.uniform_len < (1u << 24) && p.coop_lines &&
                 p.uniform_len * (uint64_t)p.n < 0xFFFFFF00ull)
                 hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 4>), dim3(full), dim3(kWG), 0, s, q);
