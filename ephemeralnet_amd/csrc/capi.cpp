@@ -70,6 +70,11 @@ enet::RecParams rec_params(const enet_records* r) {
     p.coop = (int)enet::staging_variant();
     // variant 4 = variant 1 without line-aligned staging of unaligned uniform batches
     p.coop_lines = p.coop == 1 ? 1 : 0;
+    static const int nt = [] {
+        const char* e = std::getenv("ENET_NT_STORES");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    p.nt_stores = nt;
     if (p.coop == 4) p.coop = 1;
     // COOP 3 addresses the arena with 32-bit offsets
     if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;

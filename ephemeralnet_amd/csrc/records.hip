@@ -89,6 +89,20 @@ constexpr uint32_t kStage = 2;                 // blocks per lane per cooperativ
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
 constexpr uint32_t kRing = 272;                // COOP 4: two-line ring (256 B) + 16 B pad per owner
 
+// Streaming output store: the kernel never reads its outputs back, so stores that fill whole
+// 128-byte lines are non-temporal (global_store ... nt) instead of being kept dirty in the per-XCD
+// L2 until the end-of-kernel write-back (C2 seal kernel 150 -> 142 us, tools/nt_ab.sh).  Stores
+// covering partial lines stay cached (nt there costs up to 35 %: the halves are not merged).
+typedef uint32_t enet_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_stream(uint8_t* p, uint4 v, bool nt = true) {
+    if (nt) {
+        enet_u32x4 w = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(w, reinterpret_cast<enet_u32x4*>(p));
+    } else {
+        *reinterpret_cast<uint4*>(p) = v;
+    }
+}
+
 template <int LOGP, int MODE, int FRAME, int COOP>
 __device__ __forceinline__ void records_body(const RecParams& p) {
     constexpr uint32_t P = 1u << LOGP;
@@ -231,6 +245,9 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         }
         const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
         uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
+        // every owner run covers whole aligned 64-byte halves of lines (uniform test)
+        const bool lines_whole = p.nt_stores && (Lu & 63u) == 0 && ((64ull * B) & 63u) == 0 &&
+                                 (reinterpret_cast<uintptr_t>(obase) & 63u) == 0;
         uint8_t* wslab = slab + wbase * kRun;
         uint8_t* myrun = slab + threadIdx.x * kRun;
         const uint32_t msw = (lane >> 1) & 7u;
@@ -299,7 +316,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
-                *reinterpret_cast<uint4*>(obase + off[i] + adv) = v;
+                store_stream(obase + off[i] + adv, v, lines_whole);
             }
             ENET_WAVE_LDS_SYNC();
             // (a) land the next stage in the slab
@@ -485,9 +502,9 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         auto store_inner = [&](uint32_t t) {  // line t, 1 <= t <= S-2: complete in every record
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                *reinterpret_cast<uint4*>(oal + (roff[i] + 128u * t + 16u * kk)) =
-                    *reinterpret_cast<const uint4*>(wslab + (8u * i + (lane >> 3)) * kRing +
-                                                    128u * (t & 1u) + 16u * kk);
+                store_stream(oal + (roff[i] + 128u * t + 16u * kk),
+                             *reinterpret_cast<const uint4*>(wslab + (8u * i + (lane >> 3)) * kRing +
+                                                             128u * (t & 1u) + 16u * kk));
         };
         auto store_line = [&](uint32_t t) {  // ring slot t % 2 -> line t, this record's bytes only
 #pragma unroll
@@ -501,7 +518,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
                     wslab + (8u * i + (lane >> 3)) * kRing + 128u * (t & 1u) + c0);
                 uint8_t* q = oal + (roff[i] + 128u * t + c0);
                 if (c0 >= lo && c0 + 16u <= hi) {
-                    *reinterpret_cast<uint4*>(q) = v;
+                    store_stream(q, v);
                 } else {  // a record-boundary chunk: its dwords in [lo, hi) only
                     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
