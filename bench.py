@@ -533,7 +533,7 @@ def main():
                     ops = k["SQ_INSTS_VALU"] * 64
                     valu["lane_ops_Tps"] = round(ops / dom_s / 1e12, 2)
                     valu["issue_peak_Tps"] = VALU_ISSUE_PEAK_TOPS
-                    valu["instr_per_64B_block"] = round(ops / 64 / blocks, 1)
+                    valu["instr_per_64B_block"] = round(ops / blocks, 1)  # lane instructions
                     valu["cycles_per_instr_per_simd_at_2.4GHz"] = round(
                         dom_s * 2.4e9 * 1024 / k["SQ_INSTS_VALU"], 2)
                     valu["pmc_source"] = pmc_note

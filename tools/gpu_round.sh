@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU session producing the round's evidence under gpurun_out/r$R/: GPU parity suite, the
-# default bench line, side configs/modes, rocprofv3 kernel stats, and PMC passes.
+# default bench line, side configs/modes, the torchrun launch path, rocprofv3 kernel stats, and
+# PMC passes (C2 and C3).
 # usage (on the box, from the repo root): bash tools/gpu_round.sh 01
 set -euo pipefail
 R=${1:-01}
@@ -14,16 +15,22 @@ tail -2 $O/pytest_gpu.log
 step bench default
 timeout -k 10 240 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
+step torchrun path
+timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 50 --warmup 10 --no-cpu-baseline > $O/bench_torchrun.json 2> $O/bench_torchrun.err
+cat $O/bench_torchrun.json
 step side configs
 : > $O/side.jsonl
 for args in "--records 1048576 --record-bytes 1500" "--records 32768 --record-bytes 65536" \
-            "--mode xor" "--mode wire" "--mode store" "--e2e" "--c5"; do
+            "--mode xor" "--mode wire" "--mode store" "--mode pow --cpu-seconds 5" \
+            "--mode pow --pow-schedule 0 --no-cpu-baseline" "--e2e" "--c5"; do
   step "  $args"
-  timeout -k 10 240 python bench.py --no-cpu-baseline --steps 100 --warmup 20 $args >> $O/side.jsonl 2>> $O/side.err
+  timeout -k 10 240 python bench.py --steps 100 --warmup 20 $(case "$args" in *pow*) echo "--steps 10 --warmup 3";; esac) $(case "$args" in *pow*) ;; *) echo --no-cpu-baseline;; esac) $args >> $O/side.jsonl 2>> $O/side.err
 done
 step rocprof stats
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 > $O/prof_bench.json 2> $O/prof.err
-find $O/prof -name "*stats*" | head
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3.json 2>> $O/prof.err
+find $O/prof $O/prof_c3 -name "*stats*" | head
 step pmc
 timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc.log 2>&1
+timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3 --summary $O/pmc_c3_summary.json --config "{\"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3.log 2>&1
 step done
