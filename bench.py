@@ -140,6 +140,61 @@ def cpu_baseline(record_bytes: int, budget_s: float) -> dict:
     }
 
 
+def ref_lib():
+    """oracle/_ref/libenet_ref.so: the reference's own src/crypto + StoreProof.cpp compiled in the
+    build container (oracle/Makefile ref) -- travels with the tree; None when absent."""
+    import ctypes as C
+    path = os.path.join(ROOT, "oracle", "_ref", "libenet_ref.so")
+    if not os.path.exists(path):
+        return None
+    lib = C.CDLL(path)
+    lib.ref_bench_frames.argtypes = [C.c_void_p] * 3 + [C.c_size_t, C.c_size_t, C.c_int, C.c_void_p]
+    lib.ref_bench_store_pow.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint8, C.c_uint64,
+                                        C.c_int, C.POINTER(C.c_uint64)]
+    lib.ref_bench_store_pow.restype = C.c_double
+    return lib
+
+
+def cpu_reference_frames(record_bytes: int, budget_s: float) -> dict | None:
+    """The reference itself (oracle/_ref: src/crypto ChaCha20 + HmacSha256 as compiled from
+    /root/reference) running its own record construction -- encode_signed's HMAC + ChaCha20 at
+    counter 0 and the inverse with verification (Message.cpp:305-328, SessionManager.cpp:362-374,
+    815-822) -- over records of the same length on the host cores.  Reported next to the AEAD
+    baseline because the reference has no Poly1305."""
+    import ctypes as C
+
+    import numpy as np
+    lib = ref_lib()
+    if lib is None:
+        return None
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    L = record_bytes
+    n = 128 * threads
+    rng = np.random.default_rng(3)
+    pt = rng.integers(0, 256, n * L, dtype=np.uint8)
+    keys = rng.integers(0, 256, n * 32, dtype=np.uint8)
+    nonces = rng.integers(0, 256, n * 12, dtype=np.uint8)
+    secs = (C.c_double * 2)()
+    total_s, reps = 0.0, 0
+    t_start = time.perf_counter()
+    while True:
+        fails = lib.ref_bench_frames(pt.ctypes.data, keys.ctypes.data, nonces.ctypes.data, n, L,
+                                     threads, secs)
+        assert fails == 0
+        total_s += secs[0] + secs[1]
+        reps += 1
+        if time.perf_counter() - t_start > budget_s or reps >= 64:
+            break
+    return {"value": round(reps * n * L / total_s / 2**30, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"{reps} x {n} records x {L} B, reference frame seal+open (HMAC-SHA256 + "
+                      f"ChaCha20, oracle/_ref compiled from src/crypto), {threads} threads"}
+
+
 def e2e(args) -> dict:
     """Seal and open with the data starting and ending in pinned host memory, as the reference's
     socket/relay path does, through the library's host pipeline (enet_pipeline_aead_*: chunks
@@ -351,22 +406,33 @@ def pow_bench(args) -> dict:
         if not args.no_cpu_baseline and world == 1:
             import ctypes as C
 
-            import oracle
             threads = max(1, min(16, len(os.sched_getaffinity(0))))
             m = 64 * threads
-            pre_h = np.frombuffer(os.urandom(m * plen), dtype=np.uint8).copy()
-            off_h = np.arange(0, (m + 1) * plen, plen, dtype=np.uint64)
             cpu_att = max(256, int(args.cpu_seconds * 2e6 / m))  # ~2 M hashes/s per thread budget
-            hh = C.c_uint64()
-            secs = oracle.lib().orc_bench_pow(pre_h.ctypes.data_as(C.c_void_p),
-                                              off_h.ctypes.data_as(C.c_void_p), m, 24, cpu_att,
-                                              threads, C.byref(hh))
+            lib = ref_lib() if sched == 1 else None
+            if lib is not None:  # the reference's own compute_store_pow (StoreProof.cpp:123-146)
+                found = C.c_uint64()
+                secs = lib.ref_bench_store_pow(os.urandom(32 * m), m, 4096, 24, cpu_att, threads,
+                                               C.byref(found))
+                hashes = m * (cpu_att + 1)  # not-found jobs (found ~1e-4) scan every attempt
+                kind, what = "reference", ("security::compute_store_pow from oracle/_ref (compiled "
+                                           "src/security/StoreProof.cpp + src/crypto/Sha256.cpp)")
+            else:
+                import oracle
+                pre_h = np.frombuffer(os.urandom(m * plen), dtype=np.uint8).copy()
+                off_h = np.arange(0, (m + 1) * plen, plen, dtype=np.uint64)
+                hh = C.c_uint64()
+                secs = oracle.lib().orc_bench_pow(pre_h.ctypes.data_as(C.c_void_p),
+                                                  off_h.ctypes.data_as(C.c_void_p), m, 24, cpu_att,
+                                                  threads, C.byref(hh))
+                hashes = hh.value
+                kind, what = "port", ("oracle/enet_oracle.c orc_pow_search, byte-wise SHA-256 like "
+                                      "src/crypto/Sha256.cpp, -O2")
             out["cpu_baseline"] = {
-                "value": round(hh.value / secs / 1e9, 5), "unit": "G candidates/s", "cores": threads,
-                "kind": "port",
-                "sample": f"{m} node-schedule jobs x {cpu_att} attempts, {plen}-byte prefixes "
-                          "(oracle/enet_oracle.c orc_pow_search, byte-wise SHA-256 like "
-                          "src/crypto/Sha256.cpp, -O2)"}
+                "value": round(hashes / secs / 1e9, 5), "unit": "G candidates/s", "cores": threads,
+                "kind": kind,
+                "sample": f"{m} {'store' if sched else 'handshake'}-PoW jobs x {cpu_att} attempts at "
+                          f"difficulty 24 ({what})"}
     if world > 1:
         dist.destroy_process_group()
     return out
@@ -578,7 +644,15 @@ def main():
             "valu_roofline": valu,
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
+            if args.mode == "wire":  # the same workload through the reference itself
+                ref = cpu_reference_frames(L, args.cpu_seconds)
+                if ref is not None:
+                    out["cpu_baseline"] = ref
+            else:
+                out["cpu_baseline"] = cpu_baseline(L, args.cpu_seconds)
+                ref = cpu_reference_frames(L, args.cpu_seconds / 2)
+                if ref is not None:
+                    out["cpu_reference"] = ref
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

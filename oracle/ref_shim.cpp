@@ -14,7 +14,9 @@
 #include "ephemeralnet/security/StoreProof.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <limits>
 #include <random>
@@ -200,6 +202,70 @@ int64_t ref_keymanager_rotate(const uint8_t* secret, int64_t now_ns, uint8_t* ou
     if (!key) return -1;
     std::memcpy(out, key->data(), 32);
     return now_ns;
+}
+
+// CPU baseline with the reference itself (bench.py): the reference's frame construction over n
+// records of len bytes -- seal = HmacSha256::compute(key, m) + ChaCha20::apply(key, nonce, m || mac)
+// (Message.cpp:305-311 + SessionManager.cpp:362-374), open = apply + HmacSha256::verify
+// (SessionManager.cpp:815-822 + Message.cpp:313-328) -- on `threads` std::threads.  Seconds of
+// seal and open in secs[0..1]; returns the number of failed opens.
+int ref_bench_frames(const uint8_t* pt, const uint8_t* keys, const uint8_t* nonces, size_t n, size_t len,
+                     int threads, double* secs) {
+    if (threads < 1) threads = 1;
+    std::vector<std::vector<uint8_t>> bodies(n);
+    std::atomic<int> fails{0};
+    for (int phase = 0; phase < 2; ++phase) {
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t) {
+            th.emplace_back([&, t] {
+                for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+                    crypto::Key k{};
+                    crypto::Nonce nn{};
+                    std::memcpy(k.bytes.data(), keys + 32 * i, 32);
+                    std::memcpy(nn.bytes.data(), nonces + 12 * i, 12);
+                    const std::span<const uint8_t> key(k.bytes);
+                    if (phase == 0) {
+                        std::vector<uint8_t> signed_msg(pt + len * i, pt + len * (i + 1));
+                        const auto mac = crypto::HmacSha256::compute(key, signed_msg);
+                        signed_msg.insert(signed_msg.end(), mac.begin(), mac.end());
+                        crypto::ChaCha20::apply(k, nn, signed_msg, bodies[i], 0);
+                    } else {
+                        std::vector<uint8_t> plain;
+                        crypto::ChaCha20::apply(k, nn, bodies[i], plain, 0);
+                        const std::span<const uint8_t> all(plain);
+                        if (!crypto::HmacSha256::verify(key, all.first(len), all.subspan(len))) ++fails;
+                    }
+                }
+            });
+        }
+        for (auto& x : th) x.join();
+        secs[phase] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return fails.load();
+}
+
+// security::compute_store_pow on `threads` std::threads over n inputs (chunk ids [n][32], payload
+// size, no hint) at `difficulty` with max_attempts each; returns seconds, *found = jobs that found.
+double ref_bench_store_pow(const uint8_t* chunk_ids, size_t n, uint64_t payload_size, uint8_t difficulty,
+                           uint64_t max_attempts, int threads, uint64_t* found) {
+    if (threads < 1) threads = 1;
+    std::atomic<uint64_t> f{0};
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < threads; ++t) {
+        th.emplace_back([&, t] {
+            for (size_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+                security::StoreWorkInput in{};
+                std::memcpy(in.chunk_id.data(), chunk_ids + 32 * i, 32);
+                in.payload_size = payload_size;
+                if (security::compute_store_pow(in, difficulty, max_attempts)) ++f;
+            }
+        });
+    }
+    for (auto& x : th) x.join();
+    *found = f.load();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // extern "C"

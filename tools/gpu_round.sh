@@ -21,10 +21,10 @@ cat $O/bench_torchrun.json
 step side configs
 : > $O/side.jsonl
 for args in "--records 1048576 --record-bytes 1500" "--records 32768 --record-bytes 65536" \
-            "--mode xor" "--mode wire" "--mode store" "--mode pow --cpu-seconds 5" \
+            "--mode xor" "--mode wire --cpu-seconds 5" "--mode store" "--mode pow --cpu-seconds 5" \
             "--mode pow --pow-schedule 0 --no-cpu-baseline" "--e2e" "--c5"; do
   step "  $args"
-  timeout -k 10 240 python bench.py --steps 100 --warmup 20 $(case "$args" in *pow*) echo "--steps 10 --warmup 3";; esac) $(case "$args" in *pow*) ;; *) echo --no-cpu-baseline;; esac) $args >> $O/side.jsonl 2>> $O/side.err
+  timeout -k 10 240 python bench.py --steps 100 --warmup 20 $(case "$args" in *pow*) echo "--steps 10 --warmup 3";; esac) $(case "$args" in *pow*|*wire*) ;; *) echo --no-cpu-baseline;; esac) $args >> $O/side.jsonl 2>> $O/side.err
 done
 step rocprof stats
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 > $O/prof_bench.json 2> $O/prof.err
