@@ -68,13 +68,26 @@ enet::RecParams rec_params(const enet_records* r) {
     if (r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint)
         p.uniform_len = r->max_len_hint;
     p.coop = (int)enet::staging_variant();
-    // variant 4 = variant 1 without line-aligned staging of unaligned uniform batches
-    p.coop_lines = p.coop == 1 ? 1 : 0;
+    // variant 1 (default): line staging for unaligned one-lane records, lockstep keystream in
+    // 512-thread workgroups otherwise; 4 = plain run staging (neither); 5 = lockstep run staging
+    const bool dflt = p.coop == 1;
+    p.coop_lines = dflt ? 1 : 0;
     static const int nt = [] {
         const char* e = std::getenv("ENET_NT_STORES");
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.nt_stores = nt;
+    static const int lock = [] {
+        const char* e = std::getenv("ENET_LOCKSTEP");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    p.lockstep = dflt ? lock : 0;
+    // ENET_LINES_LOCKSTEP=1: line staging in 512-thread lockstep workgroups (COOP 6, tuning)
+    static const int lines_lock = [] {
+        const char* e = std::getenv("ENET_LINES_LOCKSTEP");
+        return (e && e[0] == '1') ? 1 : 0;
+    }();
+    if (dflt && lines_lock) p.coop_lines = 2;
     if (p.coop == 4) p.coop = 1;
     // COOP 3 addresses the arena with 32-bit offsets
     if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
@@ -103,7 +116,7 @@ uint32_t staging_variant() {
         return s ? (uint32_t)std::strtoul(s, nullptr, 10) + 1u : 0u;
     }();
     if (uint32_t f = g_staging.load(std::memory_order_relaxed)) return f - 1u;
-    if (env == 1 || env == 2 || env == 4 || env == 5) return env - 1u;
+    if (env == 1 || env == 2 || env == 4 || env == 5 || env == 6) return env - 1u;
     return 1u;
 }
 
@@ -151,8 +164,8 @@ uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t ma
 }
 
 int enet_set_staging(int variant) {
-    if (variant != -1 && variant != 0 && variant != 1 && variant != 3 && variant != 4)
-        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 3 or 4");
+    if (variant != -1 && variant != 0 && variant != 1 && variant != 3 && variant != 4 && variant != 5)
+        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 3, 4 or 5");
     enet::g_staging.store((uint32_t)(variant + 1), std::memory_order_relaxed);
     return ENET_OK;
 }

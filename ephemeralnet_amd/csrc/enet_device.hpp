@@ -126,6 +126,82 @@ __device__ __forceinline__ void chacha_block2(const ChachaRecord& R, uint32_t ca
     xb[12] = b12 + cb; xb[13] = b13 + R.n[0]; xb[14] = b14 + R.n[1]; xb[15] = b15 + R.n[2];
 }
 
+// Two keystream blocks with the quarter-round steps of all 8 chains issued in a fixed order
+// (step s of every chain, then step s+1 ...) as one asm statement per instruction, and an
+// s_barrier after every 24 instructions (one add / xor / rotate step of the 8 chains).  With both
+// waves of a SIMD in one workgroup, the barrier keeps them in phase, so their full-rate v_add /
+// v_xor runs line up and pair on gfx950's dual-rate VALU instead of colliding with the other
+// wave's half-rate v_alignbit runs (tools/ubench_pair.hip: 4.29 -> 3.69 cycles per instruction).
+// Every wave of the workgroup must call this the same number of times.
+#define ENET_ASM_ADD(x, y) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(x) : "v"(y))
+#define ENET_ASM_XOR(x, y) asm volatile("v_xor_b32_e32 %0, %0, %1" : "+v"(x) : "v"(y))
+#define ENET_ASM_ROT(x, r) asm volatile("v_alignbit_b32 %0, %0, %0, %1" : "+v"(x) : "I"(32 - (r)))
+
+// one half-round (four QRs on quads Q of both blocks), steps interleaved across the 8 chains
+template <bool DIAG>
+__device__ __forceinline__ void chacha_half_lockstep(uint32_t x[32]) {
+    constexpr int C[4][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}};
+    constexpr int D[4][4] = {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
+    constexpr int R[4] = {16, 12, 8, 7};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // QR line k: (a += b, d ^= a, d <<<= 16) / (c += d, b ^= c, b <<<= 12) ...
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int* q = DIAG ? D[c & 3] : C[c & 3];
+            const int o = 16 * (c >> 2);
+            if (k % 2 == 0) ENET_ASM_ADD(x[o + q[0]], x[o + q[1]]);
+            else ENET_ASM_ADD(x[o + q[2]], x[o + q[3]]);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int* q = DIAG ? D[c & 3] : C[c & 3];
+            const int o = 16 * (c >> 2);
+            if (k % 2 == 0) ENET_ASM_XOR(x[o + q[3]], x[o + q[0]]);
+            else ENET_ASM_XOR(x[o + q[1]], x[o + q[2]]);
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int* q = DIAG ? D[c & 3] : C[c & 3];
+            const int o = 16 * (c >> 2);
+            if (k % 2 == 0) ENET_ASM_ROT(x[o + q[3]], R[k]);
+            else ENET_ASM_ROT(x[o + q[1]], R[k]);
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+}
+
+__device__ __forceinline__ void chacha_block2_lockstep(const ChachaRecord& R, uint32_t ca, uint32_t cb,
+                                                       uint32_t xa[16], uint32_t xb[16]) {
+    uint32_t a0 = kSigma0, a4 = R.k[0], a8 = R.k[4], a12 = ca;
+    uint32_t b0 = kSigma0, b4 = R.k[0], b8 = R.k[4], b12 = cb;
+    ENET_QR(a0, a4, a8, a12);
+    ENET_QR(b0, b4, b8, b12);
+    uint32_t x[32];
+    x[0] = a0; x[4] = a4; x[8] = a8; x[12] = a12;
+    x[16] = b0; x[20] = b4; x[24] = b8; x[28] = b12;
+#pragma unroll
+    for (int c = 1; c < 4; ++c) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            x[c + 4 * r] = R.pre[4 * (c - 1) + r];
+            x[16 + c + 4 * r] = R.pre[4 * (c - 1) + r];
+        }
+    }
+    chacha_half_lockstep<true>(x);
+#pragma unroll
+    for (int i = 1; i < 10; ++i) {
+        chacha_half_lockstep<false>(x);
+        chacha_half_lockstep<true>(x);
+    }
+    const uint32_t ff[16] = {kSigma0, kSigma1, kSigma2, kSigma3, R.k[0], R.k[1], R.k[2], R.k[3],
+                             R.k[4], R.k[5], R.k[6], R.k[7], 0u, R.n[0], R.n[1], R.n[2]};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        xa[i] = x[i] + (i == 12 ? ca : ff[i]);
+        xb[i] = x[16 + i] + (i == 12 ? cb : ff[i]);
+    }
+}
+
 // ----------------------------------------------------------------------------- Poly1305
 // Field elements mod 2^130-5 in five 26-bit limbs.  `Pmul` holds a multiplier and its 5x
 // multiples (2^130 == 5), so h*r needs 25 v_mad_u64_u32 and a short carry chain.

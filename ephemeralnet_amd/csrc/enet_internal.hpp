@@ -41,6 +41,7 @@ struct RecParams {
     // (COOP 4; needs 4-byte-aligned record starts and in / out starts equal mod 128)
     int coop_lines;
     int nt_stores;  // non-temporal whole-line output stores (ENET_NT_STORES=0 disables)
+    int lockstep;   // staging 1: lockstep keystream in 512-thread workgroups (ENET_LOCKSTEP=0 disables)
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the

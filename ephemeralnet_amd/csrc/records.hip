@@ -107,9 +107,14 @@ template <int LOGP, int MODE, int FRAME, int COOP>
 __device__ __forceinline__ void records_body(const RecParams& p) {
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
-    __shared__ __attribute__((aligned(16))) uint8_t slab[COOP == 4 ? kWG * kRing : COOP ? kWG * kRun : 16];
+    // COOP 5 = COOP 1 in 512-thread workgroups with the lockstep keystream (both waves of a SIMD
+    // belong to one workgroup and meet at s_barrier every 24 ChaCha instructions)
+    // (COOP 6 = COOP 4 likewise)
+    constexpr uint32_t WGS = (COOP == 5 || COOP == 6) ? 512u : (uint32_t)kWG;
+    __shared__ __attribute__((aligned(16))) uint8_t
+        slab[(COOP == 4 || COOP == 6) ? WGS * kRing : COOP ? WGS * kRun : 16];
 
-    const uint32_t gid = blockIdx.x * kWG + threadIdx.x;
+    const uint32_t gid = blockIdx.x * WGS + threadIdx.x;
     const uint32_t group = gid >> LOGP;
     const uint32_t j = gid & (P - 1);
     const bool live = group < p.n;
@@ -222,7 +227,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
     // ---- cooperative stages (uniform batches)
     uint32_t cco = cbeg;     // first block left for the per-lane fast path
     uint32_t ctail = cfast;  // first block left for the per-lane tail path
-    if (COOP == 1) {
+    if (COOP == 1 || COOP == 5) {
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t wbase = threadIdx.x & ~63u;
         const uint64_t Lu = p.uniform_len;
@@ -232,7 +237,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         const uint32_t fmin = (nfull > jl * B) ? min(B, nfull - jl * B) : 0u;
         const uint32_t Ts = fmin / kStage;
         const uint32_t kk = lane & 7u;
-        const uint32_t wgid0 = blockIdx.x * kWG + wbase;  // gid of lane 0 of this wave
+        const uint32_t wgid0 = blockIdx.x * WGS + wbase;  // gid of lane 0 of this wave
         uint64_t off[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -297,7 +302,8 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
                     poly_block64(h, PR, w2 + 16);
                 }
                 uint32_t ka[16], kb[16];
-                chacha_block2(R, c0, c0 + 1, ka, kb);
+                if (COOP == 5) chacha_block2_lockstep(R, c0, c0 + 1, ka, kb);
+                else chacha_block2(R, c0, c0 + 1, ka, kb);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
                 if (MODE == MODE_SEAL) {
@@ -436,7 +442,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             ctail = cend;
         }
     }
-    if (COOP == 4) {
+    if (COOP == 4 || COOP == 6) {
         // Line-aligned staging for uniform batches whose records are not 128-byte aligned
         // (C3: 1 500-byte records), one lane per record.  Run s of a record = record bytes
         // [128s, 128s+128) straddles two arena lines (offset d = record start mod 128), so
@@ -454,7 +460,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         const uint32_t wbase = threadIdx.x & ~63u;
         const uint32_t Lu = (uint32_t)p.uniform_len;
         const uint32_t kk = lane & 7u;
-        const uint32_t wgid0 = blockIdx.x * kWG + wbase;
+        const uint32_t wgid0 = blockIdx.x * WGS + wbase;
         const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
         uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
         const uint32_t ib = (uint32_t)reinterpret_cast<uintptr_t>(ibase);
@@ -557,7 +563,8 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             if (rl == kRun) {
                 if (MODE == MODE_OPEN) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
                 uint32_t ka[16], kb[16];
-                chacha_block2(R, c0, c0 + 1, ka, kb);
+                if (COOP == 6) chacha_block2_lockstep(R, c0, c0 + 1, ka, kb);
+                else chacha_block2(R, c0, c0 + 1, ka, kb);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
                 if (MODE == MODE_SEAL) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
@@ -878,6 +885,12 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     records_body<LOGP, MODE, FRAME, COOP>(p);
 }
 
+// 512-thread workgroups with the lockstep keystream: COOP 5 (run staging), COOP 6 (line staging)
+template <int LOGP, int MODE, int COOP>
+__global__ __launch_bounds__(512) void records_kernel_l(RecParams p) {
+    records_body<LOGP, MODE, FR_NONE, COOP>(p);
+}
+
 // COOP 3 is built to fit four waves per SIMD (<= 128 VGPRs)
 template <int LOGP, int MODE>
 __global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(4)))
@@ -891,20 +904,30 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     const uint32_t blocks = (uint32_t)((lanes + kWG - 1) / kWG);
     if (blocks == 0) return hipSuccess;
     if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop >= 1) {
-        // cooperative kernel over whole workgroups of records (no dead owners, no store
-        // predicates); the remaining records go through the per-lane kernel
-        const uint32_t per_wg = kWG >> LOGP;
+        // Cooperative kernels over whole workgroups of records (no dead owners, no store
+        // predicates); the remaining records go through the per-lane kernel.
+        // Line staging (COOP 4/6) for one-lane records that are not 64-byte multiples: 1 M
+        // records, 1 GPU, GiB/s line vs run staging -- 1500 B 746 vs 590, 1504 B 762 vs 689,
+        // 1400 B 750 vs 613; 1472 B 775 vs 789, 1536 B 835 vs 839 (tools/c3ab.sh).
+        const bool lines = LOGP == 0 && p.coop == 1 && p.coop_lines && (p.uniform_len & 63u) != 0 &&
+                           (p.uniform_len & 3u) == 0 && p.uniform_len < (1u << 24) &&
+                           p.uniform_len * (uint64_t)p.n < 0xFFFFFF00ull;
+        // Lockstep keystream in 512-thread workgroups (COOP 5) unless a plain variant is asked
+        // for: C2 837 -> 864, C4 868 -> 913 GiB/s; not with line staging, where it measured
+        // 765 -> 751 at C3 (COOP 6, kept for tuning) (tools/lock_ab.sh)
+        const bool lock = p.coop == 5 || (p.coop == 1 && p.lockstep && !lines);
+        const uint32_t wg = (lock || (lines && p.coop_lines == 2)) ? 512u : (uint32_t)kWG;
+        const uint32_t per_wg = wg >> LOGP;
         const uint32_t full = p.n / per_wg;
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            // (line staging wins whenever records are not 64-byte multiples: 1 M records, 1 GPU,
-            // GiB/s line vs run staging -- 1500 B 746 vs 590, 1504 B 762 vs 689, 1400 B 750 vs
-            // 613; 1472 B 775 vs 789, 1536 B 835 vs 839: tools/c3ab.sh)
-            if (LOGP == 0 && p.coop == 1 && (p.uniform_len & 63u) != 0 && (p.uniform_len & 3u) == 0 &&
-                p.uniform_len < (1u << 24) && p.coop_lines &&
-                p.uniform_len * (uint64_t)p.n < 0xFFFFFF00ull)
+            if (lines && p.coop_lines == 2)
+                hipLaunchKernelGGL((records_kernel_l<0, MODE, 6>), dim3(full), dim3(512), 0, s, q);
+            else if (lines)
                 hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 4>), dim3(full), dim3(kWG), 0, s, q);
+            else if (lock)
+                hipLaunchKernelGGL((records_kernel_l<LOGP, MODE, 5>), dim3(full), dim3(512), 0, s, q);
             else if (p.coop == 3)
                 hipLaunchKernelGGL((records_kernel_w4<LOGP, MODE>), dim3(full), dim3(kWG), 0, s, q);
             else

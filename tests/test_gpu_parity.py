@@ -477,7 +477,7 @@ def test_wire_frames_random_vs_oracle(enet, lanes):
 
 
 # ------------------------------------------------------------------------------ uniform (COOP)
-@pytest.mark.parametrize("staging", [1, 3, 0, 4])
+@pytest.mark.parametrize("staging", [1, 3, 0, 4, 5])
 @pytest.mark.parametrize("L,n,lanes", [(1500, 1000, 1), (1500, 517, 2), (4096, 300, 2),
                                        (4096, 129, 4), (65536, 40, 8), (65536, 33, 16),
                                        (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1),
