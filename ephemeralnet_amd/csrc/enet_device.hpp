@@ -166,7 +166,10 @@ __device__ __forceinline__ void chacha_half_lockstep(uint32_t x[32]) {
             if (k % 2 == 0) ENET_ASM_ROT(x[o + q[3]], R[k]);
             else ENET_ASM_ROT(x[o + q[1]], R[k]);
         }
-        __builtin_amdgcn_s_barrier();
+#ifndef ENET_LOCK_EVERY
+#define ENET_LOCK_EVERY 1
+#endif
+        if ((k + 1) % ENET_LOCK_EVERY == 0) __builtin_amdgcn_s_barrier();
     }
 }
 

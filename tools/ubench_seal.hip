@@ -42,6 +42,40 @@ __global__ __launch_bounds__(256) void k_stage(uint32_t* out, int stages, uint32
     out[t] = acc;
 }
 
+// The same stage body with the lockstep keystream (512-thread workgroups, both waves of a SIMD
+// in one workgroup, s_barrier every 24 ChaCha instructions) -- the records kernel's default.
+template <int POLY>
+__global__ __launch_bounds__(512) void k_stage_l(uint32_t* out, int stages, uint32_t seed) {
+    const uint32_t t = blockIdx.x * 512 + threadIdx.x;
+    uint32_t kw[8], nw[3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kw[i] = seed * (i + 3) ^ t;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) nw[i] = seed + i * t;
+    ChachaRecord R;
+    chacha_record_init(R, kw, nw);
+    PolyR32 PR = polyr32_make(kw[0], kw[1], kw[2], kw[3]);
+    uint32_t h[5] = {0, 0, 0, 0, 0};
+    uint32_t w2[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) w2[i] = t * (i + 1);
+    for (int st = 0; st < stages; ++st) {
+        uint32_t ka[16], kb[16];
+        chacha_block2_lockstep(R, 2 * st, 2 * st + 1, ka, kb);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+        if (POLY) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                poly32_block(h, PR, w2[4 * u], w2[4 * u + 1], w2[4 * u + 2], w2[4 * u + 3], 1u);
+        }
+    }
+    uint32_t acc = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc ^= w2[i];
+    out[t] = acc;
+}
+
 int coop_main();
 int main() {
     if (coop_main()) return 1;
@@ -72,6 +106,24 @@ int main() {
                    poly ? "chacha2+poly8" : "chacha2", occ, blocks / (ms * 1e6),
                    ms * 1e-3 * 2.4e9 / (occ * (double)stages));
         }
+    }
+    for (int poly = 0; poly < 2; ++poly) {  // lockstep: 512-thread workgroups, 2 waves per SIMD
+        const int stages = 200;
+        auto launch = [&](int s) {
+            if (poly) hipLaunchKernelGGL(k_stage_l<1>, dim3(256), dim3(512), 0, 0, d, s, 1u);
+            else hipLaunchKernelGGL(k_stage_l<0>, dim3(256), dim3(512), 0, 0, d, s, 1u);
+        };
+        launch(10);
+        hipEventRecord(e0);
+        launch(stages);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        const double blocks = 256.0 * 512 * stages * 2;
+        printf("{\"body\":\"%s lockstep\",\"waves_per_simd\":2,\"Gblocks_per_s\":%.2f,"
+               "\"cycles_per_wave_stage_at_2.4GHz\":%.0f}\n",
+               poly ? "chacha2+poly8" : "chacha2", blocks / (ms * 1e6), ms * 1e-3 * 2.4e9 / (2.0 * stages));
     }
     return 0;
 }
