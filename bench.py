@@ -589,8 +589,11 @@ def main():
             with open(PMC_FILE) as f:
                 pmc = json.load(f)
             lanes = E.lanes_per_record(n, n * L, L)
-            want = f"records_kernel<{lanes.bit_length() - 1}, {1 if dom == 'seal' else 2}, 0, 1>"
-            k = next((v for name, v in pmc.get("kernels", {}).items() if want in name), None)
+            lg, md = lanes.bit_length() - 1, 1 if dom == "seal" else 2
+            # the lockstep kernel (default for 64-byte-multiple records), else the 256-thread one
+            k = None
+            for want in (f"records_kernel_l<{lg}, {md}, 5>", f"records_kernel<{lg}, {md}, 0, 1>"):
+                k = k or next((v for name, v in pmc.get("kernels", {}).items() if want in name), None)
             if k and args.mode == "aead" and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
                 pmc_note = os.path.relpath(PMC_FILE, ROOT)

@@ -23,7 +23,8 @@ from dataclasses import dataclass
 from typing import Optional, Sequence
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG, "libenet_crypto.so")
+# ENET_LIB_PATH: a differently-built copy of the library (tuning builds under tools/)
+LIB_PATH = os.environ.get("ENET_LIB_PATH") or os.path.join(PKG, "libenet_crypto.so")
 
 ENET_OK = 0
 
