@@ -10,7 +10,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libenet_crypto.so")
-SOURCES = ["records.hip", "sha.hip", "pow.hip", "capi.cpp", "crypto_api.cpp", "pipeline.cpp"]
+SOURCES = ["records.hip", "sha.hip", "pow.hip", "frames.hip", "capi.cpp", "crypto_api.cpp", "pipeline.cpp"]
 HEADERS = ["enet_device.hpp", "enet_internal.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC", "-shared",

@@ -94,6 +94,53 @@ enet::RecParams rec_params(const enet_records* r) {
     return p;
 }
 
+// Uniform batches of session frames go through the fused HMAC + ChaCha20 kernel (frames.hip) in
+// whole workgroups of 256 records; the rest of the batch (and every other shape) through the
+// two-pass path (sha_kernel + records_kernel).  Returns the number of records handled (0 = none).
+// Staging variant 0 (enet_set_staging(0) / ENET_COOP=0) and ENET_FUSED_FRAMES=0 turn it off.
+uint32_t frames_fused(const enet_records* r, bool open, uint32_t hdr, uint8_t* macs, uint8_t* ok,
+                      hipStream_t st, int* err) {
+    static const bool on = [] {
+        const char* e = std::getenv("ENET_FUSED_FRAMES");
+        return !(e && e[0] == '0');
+    }();
+    *err = ENET_OK;
+    if (!on || enet::staging_variant() == 0 || r->order) return 0;
+    if (!r->max_len_hint || r->total_bytes_hint != (uint64_t)r->count * r->max_len_hint) return 0;
+    const uint64_t over = open ? 32ull + hdr : 0ull;  // frame bytes beyond the message
+    if (r->max_len_hint < over) return 0;
+    const uint64_t Lm = r->max_len_hint - over;
+    if (Lm < enet::kFrameRun || Lm % enet::kFrameRun != 0) return 0;
+    const uint32_t full = r->count / enet::kFrameRecsPerWG * enet::kFrameRecsPerWG;
+    if (!full) return 0;
+    enet::FrameFusedParams p{};
+    p.n = full;
+    p.in = r->in;
+    p.in_off = r->in_offsets;
+    p.out = r->out;
+    p.out_off = r->out_offsets;
+    p.keys = r->keys;
+    p.key_stride = r->key_stride;
+    p.nonces = r->nonces;
+    p.msg_len = Lm;
+    p.macs = macs;
+    p.ok = ok;
+    *err = hip_status(enet::launch_frames_fused(open, hdr, p, st), "fused frames launch");
+    return full;
+}
+
+// records [k, count) of r as a batch of their own (position-indexed outputs shift with them)
+enet_records tail_records(const enet_records* r, uint32_t k) {
+    enet_records q = *r;
+    q.count = r->count - k;
+    q.in_offsets += k;
+    q.out_offsets += k;
+    q.keys += (size_t)r->key_stride * k;
+    if (q.nonces) q.nonces += 12ull * k;
+    if (q.total_bytes_hint) q.total_bytes_hint = (uint64_t)q.count * r->max_len_hint;
+    return q;
+}
+
 uint32_t lanes_for(const enet_records* r) {
     return enet::choose_lanes(r->count, r->total_bytes_hint, r->max_len_hint);
 }
@@ -322,6 +369,12 @@ int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags, const 
 int enet_frame_seal_batch(const enet_records* r, void* stream) {
     if (int e = check_records(r, true)) return e;
     if (r->count == 0) return ENET_OK;
+    int fe;
+    if (uint32_t k = frames_fused(r, false, 0, nullptr, nullptr, (hipStream_t)stream, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records q = tail_records(r, k);
+        return enet_frame_seal_batch(&q, stream);
+    }
     // 1) MAC = HMAC-SHA256(K, m) written in clear at the tail of each output record
     enet::ShaParams s{};
     s.n = r->count;
@@ -344,6 +397,12 @@ int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, voi
     if (r->count == 0) return ENET_OK;
     if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "frame_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
+    int fe;
+    if (uint32_t k = frames_fused(r, true, 0, macs, ok, st, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records q = tail_records(r, k);
+        return enet_frame_open_batch(&q, macs + 32ull * k, ok + k, stream);
+    }
     // 1) decrypt: message bytes to out, MAC bytes to macs
     enet::RecParams p = rec_params(r);
     p.tag_out = macs;
@@ -419,6 +478,12 @@ int enet_wire_seal_batch(const enet_records* r, void* stream) {
     if (int e = check_records(r, true)) return e;
     if (r->count == 0) return ENET_OK;
     hipStream_t st = (hipStream_t)stream;
+    int fe;
+    if (uint32_t k = frames_fused(r, false, kWireHeader, nullptr, nullptr, st, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records q = tail_records(r, k);
+        return enet_wire_seal_batch(&q, stream);
+    }
     // 1) MAC = HMAC-SHA256(K, m) in clear at the tail of each frame body
     enet::ShaParams s{};
     s.n = r->count;
@@ -445,6 +510,12 @@ int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void
     if (int e = check_records(&q, true)) return e;
     if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "wire_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
+    int fe;
+    if (uint32_t k = frames_fused(&q, true, kWireHeader, macs, ok, st, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records t = tail_records(r, k);
+        return enet_wire_open_batch(&t, macs + 32ull * k, ok + k, stream);
+    }
     enet::RecParams p = rec_params(&q);
     p.nonces = nullptr;
     p.hdr = kWireHeader;

@@ -75,6 +75,26 @@ struct ShaParams {
 };
 hipError_t launch_sha(const ShaParams& p, hipStream_t s);
 
+// Fused HMAC-SHA256 + ChaCha20 over uniform batches of session frames (frames.hip): every
+// record holds msg_len message bytes (a multiple of kFrameRun), records are contiguous in both
+// arenas, seal writes [hdr] || ChaCha20(m || HMAC(m)) and open the reverse.
+constexpr uint32_t kFrameRecsPerWG = 256;
+constexpr uint32_t kFrameRun = 128;
+struct FrameFusedParams {
+    uint32_t n;  // records, a multiple of kFrameRecsPerWG
+    const uint8_t* in;
+    const uint64_t* in_off;
+    uint8_t* out;
+    const uint64_t* out_off;
+    const uint8_t* keys;
+    uint32_t key_stride;
+    const uint8_t* nonces;  // seal and frame open: [n][12]; wire open reads the frame header
+    uint64_t msg_len;
+    uint8_t* macs;  // open: decrypted MACs [n][32]
+    uint8_t* ok;    // open: verdicts
+};
+hipError_t launch_frames_fused(bool open, uint32_t hdr, const FrameFusedParams& p, hipStream_t s);
+
 // Proof-of-work search / check (pow.hip): SHA-256(prefix_i || BE64(candidate)).
 struct PowParams {
     uint32_t n;
