@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--pow-schedule", type=int, default=1, choices=[0, 1],
                     help="--mode pow: 1 = store PoW (mt19937_64 candidates, 44-byte prefix), "
                          "0 = handshake PoW (start + attempt, 88-byte prefix)")
+    ap.add_argument("--store-ids", default="given", choices=["given", "content"],
+                    help="store mode: caller-given chunk ids (fused kernel) or content-derived")
     ap.add_argument("--mode", default="aead", choices=["aead", "xor", "wire", "store", "pow"],
                     help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline "
                          "probe); wire = session wire frames seal+open (SURVEY 8f row 1, messages "
@@ -490,6 +492,11 @@ def main():
         wire_b = E.Batch(frames, foffs, keys, None, total_bytes_hint=n * F, max_len_hint=F)
     if args.mode == "store":
         hashes = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+        # Node::store_chunk(chunk_id, data) takes the id from its caller (ControlServer.cpp:1101
+        # derives it beforehand): "given" ids take the fused one-pass kernel; "content" ids
+        # (counter from the fresh digest) need the digest first, i.e. two passes
+        ids = (torch.randint(0, 256, (32 * n,), dtype=torch.uint8, device=dev)
+               if args.store_ids == "given" else None)
 
     def seal():
         if args.mode == "aead":
@@ -497,7 +504,7 @@ def main():
         elif args.mode == "wire":
             E.wire_seal(seal_b, frames, foffs, stream=stream)
         elif args.mode == "store":
-            E.chunk_store(seal_b, ct, hashes, stream=stream)
+            E.chunk_store(seal_b, ct, hashes, chunk_ids=ids, stream=stream)
         else:
             E.chacha20_xor(seal_b, ct, stream=stream)
 
@@ -507,7 +514,7 @@ def main():
         elif args.mode == "wire":
             E.wire_open(wire_b, back, offs, macs, ok, stream=stream)
         elif args.mode == "store":
-            E.chunk_fetch(open_b, back, hashes, hashes, ok, stream=stream)
+            E.chunk_fetch(open_b, back, hashes if ids is None else ids, hashes, ok, stream=stream)
         else:
             E.chacha20_xor(open_b, back, stream=stream)
 
@@ -557,7 +564,8 @@ def main():
         value = total_bytes / elapsed / 2**30
         # algorithmic HBM bytes per launch: seal 2L+64, open 2L+65 per record
         # (xor: 2L + key/nonce/counter 48; wire: frames carry 48 more bytes; store: hashes/ids)
-        seal_bytes = n * (2 * L + {"aead": 64, "xor": 48, "wire": 92, "store": 76}[args.mode])
+        seal_bytes = n * (2 * L + {"aead": 64, "xor": 48, "wire": 92, "store": 76}[args.mode]
+                          + (4 if args.mode == "store" and args.store_ids == "given" else 0))
         open_bytes = n * (2 * L + {"aead": 65, "xor": 48, "wire": 81, "store": 109}[args.mode])
         seal_gbs = seal_bytes / (seal_ms * 1e-3) / 1e9
         open_gbs = open_bytes / (open_ms * 1e-3) / 1e9
@@ -628,6 +636,7 @@ def main():
                 "record_bytes": L,
                 "lanes_per_record": E.lanes_per_record(n, n * L, L),
                 "parallelism": f"records split over {world} GPU(s), no collective",
+                **({"chunk_ids": args.store_ids} if args.mode == "store" else {}),
             },
             "seal_ms": round(seal_ms, 4),
             "open_ms": round(open_ms, 4),

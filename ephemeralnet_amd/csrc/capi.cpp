@@ -129,6 +129,41 @@ uint32_t frames_fused(const enet_records* r, bool open, uint32_t hdr, uint8_t* m
     return full;
 }
 
+// Chunk store / fetch through the fused kernel (frames.hip, CHUNK): uniform batches whose length is
+// a positive multiple of 128 B, whole workgroups of 256 records, caller-given chunk ids (a
+// content-derived counter needs the digest before the first block, so that case stays two-pass).
+// Returns the number of records handled; ENET_FUSED_CHUNKS=0 / staging variant 0 turn it off.
+uint32_t chunks_fused(const enet_records* r, bool fetch, const uint8_t* chunk_ids, uint8_t* digests,
+                      const uint8_t* expect, uint8_t* ok, hipStream_t st, int* err) {
+    static const bool on = [] {
+        const char* e = std::getenv("ENET_FUSED_CHUNKS");
+        return !(e && e[0] == '0');
+    }();
+    *err = ENET_OK;
+    if (!on || !chunk_ids || enet::staging_variant() == 0 || r->order) return 0;
+    if (!r->max_len_hint || r->total_bytes_hint != (uint64_t)r->count * r->max_len_hint) return 0;
+    const uint64_t L = r->max_len_hint;
+    if (L < enet::kFrameRun || L % enet::kFrameRun != 0) return 0;
+    const uint32_t full = r->count / enet::kFrameRecsPerWG * enet::kFrameRecsPerWG;
+    if (!full) return 0;
+    enet::FrameFusedParams p{};
+    p.n = full;
+    p.in = r->in;
+    p.in_off = r->in_offsets;
+    p.out = r->out;
+    p.out_off = r->out_offsets;
+    p.keys = r->keys;
+    p.key_stride = r->key_stride;
+    p.nonces = r->nonces;
+    p.msg_len = L;
+    p.ok = ok;
+    p.chunk_ids = chunk_ids;
+    p.digests = digests;
+    p.expect = expect;
+    *err = hip_status(enet::launch_chunks_fused(fetch, p, st), "fused chunks launch");
+    return full;
+}
+
 // records [k, count) of r as a batch of their own (position-indexed outputs shift with them)
 enet_records tail_records(const enet_records* r, uint32_t k) {
     enet_records q = *r;
@@ -431,6 +466,12 @@ int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids, uint
         return fail(ENET_EINVAL, "chunk_store: chunk_hashes NULL or misaligned");
     if (chunk_ids && !aligned4(chunk_ids)) return fail(ENET_EINVAL, "chunk_store: chunk_ids misaligned");
     hipStream_t st = (hipStream_t)stream;
+    int fe;
+    if (uint32_t k = chunks_fused(r, false, chunk_ids, chunk_hashes, nullptr, nullptr, st, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records q = tail_records(r, k);
+        return enet_chunk_store_batch(&q, chunk_ids + 32ull * k, chunk_hashes + 32ull * k, stream);
+    }
     // 1) chunk_hash = SHA-256(pt) (Node.cpp:1414; = derive_chunk_id, StoreProof.cpp:75-78)
     enet::ShaParams s{};
     s.n = r->count;
@@ -455,6 +496,13 @@ int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
     if (!chunk_ids || !aligned4(chunk_ids) || !chunk_hashes || !ok)
         return fail(ENET_EINVAL, "chunk_fetch: NULL/misaligned chunk_ids, NULL hashes or ok");
     hipStream_t st = (hipStream_t)stream;
+    int fe;
+    if (uint32_t k = chunks_fused(r, true, chunk_ids, nullptr, chunk_hashes, ok, st, &fe)) {
+        if (fe || k == r->count) return fe;
+        const enet_records q = tail_records(r, k);
+        return enet_chunk_fetch_batch(&q, chunk_ids + 32ull * k, chunk_hashes + 32ull * k, ok + k,
+                                      stream);
+    }
     // 1) decrypt_with_key (CryptoManager.cpp:49-58)
     enet::RecParams p = rec_params(r);
     p.counters = reinterpret_cast<const uint32_t*>(chunk_ids);

@@ -92,8 +92,13 @@ struct FrameFusedParams {
     uint64_t msg_len;
     uint8_t* macs;  // open: decrypted MACs [n][32]
     uint8_t* ok;    // open: verdicts
+    const uint8_t* chunk_ids;  // chunks: [n][32], start counter LE32(id[0..3])
+    uint8_t* digests;          // chunk store: SHA-256(m) [n][32]
+    const uint8_t* expect;     // chunk fetch: expected SHA-256 [n][32]
 };
 hipError_t launch_frames_fused(bool open, uint32_t hdr, const FrameFusedParams& p, hipStream_t s);
+// the same kernel for the chunk store (SHA-256 + ChaCha20) / fetch (ChaCha20 + SHA-256 check)
+hipError_t launch_chunks_fused(bool fetch, const FrameFusedParams& p, hipStream_t s);
 
 // Proof-of-work search / check (pow.hip): SHA-256(prefix_i || BE64(candidate)).
 struct PowParams {

@@ -46,7 +46,11 @@ __device__ __forceinline__ void sha_iv(uint32_t st[8]) {
 
 // OPEN: false = seal (in = m, out = [hdr] || body), true = open (in = [hdr] || body, out = m).
 // HDR: 16 = whole wire frames (nonce || BE32 length header), 0 = frame bodies.
-template <bool OPEN, int HDR>
+// CHUNK: the store / fetch pipeline instead (Node::store_chunk, src/core/Node.cpp:1414-1417;
+// Node::fetch_chunk, :1644-1655): ciphertext = ChaCha20(key, nonce, LE32(chunk_id), m) with no MAC
+// tail (CryptoManager.cpp:8-13,38-58), and the MAC waves compute the plain SHA-256(m) -- written
+// to p.digests on store, compared with p.expect on fetch (failed chunks are zeroed).
+template <bool OPEN, int HDR, bool CHUNK>
 __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[4 * 64 * kFrameRun];           // 32 KB
     __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kFrameRecsPerWG * kFrameRun];  // 64 KB
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
     const uint32_t rec = rec0 + rl;
     const uint64_t Lm = p.msg_len;
     const uint32_t Ts = (uint32_t)(Lm / kFrameRun);
-    const uint64_t Lb = Lm + 32;  // body = m || MAC
+    const uint64_t Lb = CHUNK ? Lm : Lm + 32;  // frame body = m || MAC, chunk = m
     const uint64_t Si = OPEN ? Lb + HDR : Lm;
     const uint64_t So = OPEN ? Lm : Lb + HDR;
     const uint8_t* inb = p.in + p.in_off[0];
@@ -91,6 +95,8 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
         }
         ChachaRecord R;
         chacha_record_init(R, kw, nw);
+        // ChaCha20::apply's start counter: 0 for frames, LE32(chunk_id[0..3]) for chunks (u32 wrap)
+        const uint32_t c0 = CHUNK ? ld32(p.chunk_ids + 32ull * rec) : 0u;
         // load / store instruction i serves owners 8i..8i+7 of this wave, 8 lanes x 16 B each
         const uint32_t kk = lane & 7u;
         uint64_t ioff[8], ooff[8];
@@ -141,7 +147,7 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
             if (!OPEN) put_run(pt, x);  // plaintext for the MAC lane
             {
                 uint32_t ka[16], kb[16];
-                chacha_block2(R, 2u * s, 2u * s + 1u, ka, kb);  // frames: counter 0 base
+                chacha_block2(R, c0 + 2u * s, c0 + 2u * s + 1u, ka, kb);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
             }
@@ -157,6 +163,14 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
             ENET_FR_WAVE_SYNC();
             land();
             ENET_WG_LDS_BARRIER();  // stage s plaintext is in ptb[s & 1]
+        }
+        if (CHUNK) {
+            if (OPEN) {
+                // the plaintext stores are complete before a MAC lane may zero them on failure
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                ENET_WG_LDS_BARRIER();
+            }
+            return;
         }
         uint32_t ks[16];
         chacha_block(R, (uint32_t)(Lm >> 6), ks);  // the MAC is the body's block Lm / 64
@@ -190,15 +204,18 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
         }
     } else {
         // ------------------------------------------------------------------ MAC waves
-        // HMAC-SHA256 (HmacSha256.cpp:11-39) with the 32-byte session key
+        // frames: HMAC-SHA256 (HmacSha256.cpp:11-39) with the 32-byte session key;
+        // chunks: SHA-256 (Sha256::digest, Sha256.cpp:66-132)
         uint32_t kb[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) kb[i] = bswap32(kw[i]);
         uint32_t st[8], x[16];
         sha_iv(st);
+        if (!CHUNK) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x36363636u;
-        sha256_compress(st, x);
+            for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x36363636u;
+            sha256_compress(st, x);
+        }
         for (uint32_t s = 0; s < Ts; ++s) {
             ENET_WG_LDS_BARRIER();
             const uint8_t* pt = myp + (s & 1u) * kPtbBuf;
@@ -213,14 +230,34 @@ __global__ __launch_bounds__(kFWG) void frames_fused_kernel(FrameFusedParams p) 
                 sha256_compress(st, x);
             }
         }
-        {  // padding of ipad || m: 0x80, zeros, BE64 bit length (Lm is a multiple of 64)
-            const uint64_t bits = (64ull + Lm) * 8ull;
+        {  // padding of [ipad ||] m: 0x80, zeros, BE64 bit length (Lm is a multiple of 64)
+            const uint64_t bits = ((CHUNK ? 0ull : 64ull) + Lm) * 8ull;
 #pragma unroll
             for (int i = 0; i < 16; ++i) x[i] = 0u;
             x[0] = 0x80000000u;
             x[14] = (uint32_t)(bits >> 32);
             x[15] = (uint32_t)bits;
             sha256_compress(st, x);
+        }
+        if (CHUNK) {
+            if (!OPEN) {  // chunk_hash = SHA-256(m), digest bytes big-endian
+                uint4* d = reinterpret_cast<uint4*>(p.digests + 32ull * rec);
+                d[0] = make_uint4(bswap32(st[0]), bswap32(st[1]), bswap32(st[2]), bswap32(st[3]));
+                d[1] = make_uint4(bswap32(st[4]), bswap32(st[5]), bswap32(st[6]), bswap32(st[7]));
+                return;
+            }
+            ENET_WG_LDS_BARRIER();  // the cipher waves' plaintext stores are complete
+            // hash != manifest.chunk_hash -> no plaintext (Node.cpp:1652-1655)
+            const uint8_t* e = p.expect + 32ull * rec;
+            uint32_t diff = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) diff |= ld32(e + 4 * i) ^ bswap32(st[i]);
+            p.ok[rec] = diff == 0 ? 1 : 0;
+            if (diff != 0) {
+                uint4* z = reinterpret_cast<uint4*>(outb + So * rec);
+                for (uint64_t b = 0; b < Lm / 16; ++b) z[b] = make_uint4(0u, 0u, 0u, 0u);
+            }
+            return;
         }
         uint32_t inner[8];
 #pragma unroll
@@ -265,13 +302,23 @@ hipError_t launch_frames_fused(bool open, uint32_t hdr, const FrameFusedParams& 
     const uint32_t blocks = p.n / kFrameRecsPerWG;
     if (blocks == 0) return hipSuccess;
     if (!open && hdr)
-        hipLaunchKernelGGL((frames_fused_kernel<false, 16>), dim3(blocks), dim3(kFWG), 0, s, p);
+        hipLaunchKernelGGL((frames_fused_kernel<false, 16, false>), dim3(blocks), dim3(kFWG), 0, s, p);
     else if (!open)
-        hipLaunchKernelGGL((frames_fused_kernel<false, 0>), dim3(blocks), dim3(kFWG), 0, s, p);
+        hipLaunchKernelGGL((frames_fused_kernel<false, 0, false>), dim3(blocks), dim3(kFWG), 0, s, p);
     else if (hdr)
-        hipLaunchKernelGGL((frames_fused_kernel<true, 16>), dim3(blocks), dim3(kFWG), 0, s, p);
+        hipLaunchKernelGGL((frames_fused_kernel<true, 16, false>), dim3(blocks), dim3(kFWG), 0, s, p);
     else
-        hipLaunchKernelGGL((frames_fused_kernel<true, 0>), dim3(blocks), dim3(kFWG), 0, s, p);
+        hipLaunchKernelGGL((frames_fused_kernel<true, 0, false>), dim3(blocks), dim3(kFWG), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunks_fused(bool fetch, const FrameFusedParams& p, hipStream_t s) {
+    const uint32_t blocks = p.n / kFrameRecsPerWG;
+    if (blocks == 0) return hipSuccess;
+    if (fetch)
+        hipLaunchKernelGGL((frames_fused_kernel<true, 0, true>), dim3(blocks), dim3(kFWG), 0, s, p);
+    else
+        hipLaunchKernelGGL((frames_fused_kernel<false, 0, true>), dim3(blocks), dim3(kFWG), 0, s, p);
     return hipGetLastError();
 }
 
