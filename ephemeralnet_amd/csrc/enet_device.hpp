@@ -419,10 +419,11 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
             w[i & 15] = wi;
         }
         const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t ch = (e & f) ^ (~e & g);
+        const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // (e & f) ^ (~e & g)
         const uint32_t t1 = h + S1 + ch + kSha256K[i] + wi;
         const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        // majority in one v_bitop3 (the compiler's own form takes three VALU ops)
+        const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
