@@ -141,7 +141,9 @@ ENET_API int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tag
  *        CryptoManager.cpp:38-46) where chunk_id_i = chunk_ids[i], or the fresh chunk_hashes[i]
  *        when chunk_ids == NULL (the daemon derives ids from content, ControlServer.cpp:1101).
  * fetch: out_i = ChaCha20(key_i, nonce_i, LE32(chunk_ids[i][0..3]), in_i); ok[i] =
- *        SHA-256(out_i) == chunk_hashes[i]; on mismatch out_i is zeroed (no plaintext). */
+ *        SHA-256(out_i) == chunk_hashes[i]; on mismatch out_i is zeroed (no plaintext).
+ * Uniform batches (length a multiple of 128 B) with chunk_ids given take one fused pass over
+ * HBM (hash and cipher together); content-derived ids need the digest first (two passes). */
 ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids,
                                     uint8_t* chunk_hashes, void* stream);
 ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
