@@ -60,7 +60,10 @@ EXPORTS = [
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
     "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_host_alloc",
-    "enet_host_free", "enet_pow_search_batch", "enet_pow_check_batch", "enet_session_key_batch",
+    "enet_host_free", "enet_pipeline_group_create", "enet_pipeline_group_destroy",
+    "enet_pipeline_group_size", "enet_pipeline_group_chacha20_xor", "enet_pipeline_group_aead_seal",
+    "enet_pipeline_group_aead_open", "enet_pipeline_group_aead_hmac_seal",
+    "enet_pipeline_group_aead_hmac_open", "enet_pow_search_batch", "enet_pow_check_batch", "enet_session_key_batch",
 ]
 
 POW_NODE = 0   # candidates start + attempt (Node.cpp announce / handshake)
@@ -108,6 +111,16 @@ def lib() -> C.CDLL:
         L.enet_pipeline_aead_open.argtypes = [vp, rp, vp, vp]
         L.enet_pipeline_aead_hmac_seal.argtypes = [vp, rp, vp, vp]
         L.enet_pipeline_aead_hmac_open.argtypes = [vp, rp, vp, vp, vp]
+        L.enet_pipeline_group_create.argtypes = [vp, u32, u64, u32]
+        L.enet_pipeline_group_create.restype = vp
+        L.enet_pipeline_group_destroy.argtypes = [vp]
+        L.enet_pipeline_group_size.argtypes = [vp]
+        L.enet_pipeline_group_size.restype = u32
+        L.enet_pipeline_group_chacha20_xor.argtypes = [vp, rp, vp]
+        L.enet_pipeline_group_aead_seal.argtypes = [vp, rp, vp]
+        L.enet_pipeline_group_aead_open.argtypes = [vp, rp, vp, vp]
+        L.enet_pipeline_group_aead_hmac_seal.argtypes = [vp, rp, vp, vp]
+        L.enet_pipeline_group_aead_hmac_open.argtypes = [vp, rp, vp, vp, vp]
         L.enet_host_alloc.argtypes = [u64]
         L.enet_host_alloc.restype = vp
         L.enet_host_free.argtypes = [vp]
@@ -347,6 +360,7 @@ class Pipeline:
     and every output lives in HOST memory (pinned, e.g. tensor.pin_memory(), for asynchronous
     DMA); the library cuts the batch into chunks and overlaps H2D, kernels and D2H over several
     HIP streams.  Calls block until the outputs are in host memory."""
+    _prefix = "enet_pipeline_"
 
     def __init__(self, device: int = 0, chunk_bytes: int = 0, streams: int = 0):
         self._p = lib().enet_pipeline_create(device, chunk_bytes, streams)
@@ -354,9 +368,12 @@ class Pipeline:
             raise EnetError("enet_pipeline_create failed: "
                             + lib().enet_last_error().decode(errors="replace"))
 
+    def _fn(self, op: str):
+        return getattr(lib(), self._prefix + op), self._prefix + op
+
     def close(self) -> None:
         if self._p:
-            lib().enet_pipeline_destroy(self._p)
+            getattr(lib(), self._prefix + "destroy")(self._p)
             self._p = None
 
     def __enter__(self):
@@ -371,27 +388,42 @@ class Pipeline:
         except Exception:
             pass
 
-    def chacha20_xor(self, b: Batch, out, counters=None) -> None:
+    def _run(self, op: str, b: Batch, out, *ptrs) -> None:
         r = b.records(out, b.offsets)
-        _check(lib().enet_pipeline_chacha20_xor(self._p, C.byref(r), _ptr(counters)),
-               "enet_pipeline_chacha20_xor")
+        fn, name = self._fn(op)
+        _check(fn(self._p, C.byref(r), *[_ptr(p) for p in ptrs]), name)
+
+    def chacha20_xor(self, b: Batch, out, counters=None) -> None:
+        self._run("chacha20_xor", b, out, counters)
 
     def aead_seal(self, b: Batch, out, tags) -> None:
-        r = b.records(out, b.offsets)
-        _check(lib().enet_pipeline_aead_seal(self._p, C.byref(r), _ptr(tags)),
-               "enet_pipeline_aead_seal")
+        self._run("aead_seal", b, out, tags)
 
     def aead_open(self, b: Batch, out, tags, ok) -> None:
-        r = b.records(out, b.offsets)
-        _check(lib().enet_pipeline_aead_open(self._p, C.byref(r), _ptr(tags), _ptr(ok)),
-               "enet_pipeline_aead_open")
+        self._run("aead_open", b, out, tags, ok)
 
     def aead_hmac_seal(self, b: Batch, out, tags, macs) -> None:
-        r = b.records(out, b.offsets)
-        _check(lib().enet_pipeline_aead_hmac_seal(self._p, C.byref(r), _ptr(tags), _ptr(macs)),
-               "enet_pipeline_aead_hmac_seal")
+        self._run("aead_hmac_seal", b, out, tags, macs)
 
     def aead_hmac_open(self, b: Batch, out, tags, macs, ok) -> None:
-        r = b.records(out, b.offsets)
-        _check(lib().enet_pipeline_aead_hmac_open(self._p, C.byref(r), _ptr(tags), _ptr(macs),
-                                                  _ptr(ok)), "enet_pipeline_aead_hmac_open")
+        self._run("aead_hmac_open", b, out, tags, macs, ok)
+
+
+class PipelineGroup(Pipeline):
+    """Host-resident batches over several devices of one node (enet_pipeline_group_*): the batch
+    is cut into contiguous record ranges balanced by input bytes, one pipeline and host thread
+    per device, no collective.  devices=None: every visible device; a device may repeat."""
+    _prefix = "enet_pipeline_group_"
+
+    def __init__(self, devices=None, chunk_bytes: int = 0, streams: int = 0):
+        devs = list(devices or [])
+        arr = (C.c_int * max(len(devs), 1))(*devs)
+        self._p = lib().enet_pipeline_group_create(arr if devs else None, len(devs), chunk_bytes,
+                                                   streams)
+        if not self._p:
+            raise EnetError("enet_pipeline_group_create failed: "
+                            + lib().enet_last_error().decode(errors="replace"))
+
+    @property
+    def size(self) -> int:
+        return int(lib().enet_pipeline_group_size(self._p))

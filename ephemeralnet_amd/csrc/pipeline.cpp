@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "enet_crypto.h"
@@ -322,7 +323,131 @@ int run(enet_pipeline* pp, Op op, const enet_records* r, const uint32_t* counter
 
 }  // namespace
 
+// Several devices of one node: one pipeline, host thread and set of streams per
+// device; a batch is cut into contiguous record ranges balanced by input bytes, so a mixed
+// 512 B - 64 KiB batch (C5) gives every device the same payload; no collective -- each range's
+// tags / MACs / ok land at their positions in the caller's arrays.
+struct enet_pipeline_group {
+    std::vector<enet_pipeline*> pipes;
+};
+
+namespace {
+
+int group_run(enet_pipeline_group* g, Op op, const enet_records* r, const uint32_t* counters,
+              const uint8_t* tags_in, const uint8_t* macs_in, uint8_t* tags_out, uint8_t* macs_out,
+              uint8_t* ok_out) {
+    if (!g || g->pipes.empty()) return perr(ENET_EINVAL, "pipeline group is NULL or empty");
+    if (!r) return perr(ENET_EINVAL, "records descriptor is NULL");
+    const uint32_t n = r->count;
+    if (n == 0) return ENET_OK;
+    if (!r->in_offsets || !r->out_offsets) return perr(ENET_EINVAL, "records: NULL offsets");
+    if (r->order) return perr(ENET_EINVAL, "pipeline group: order is not supported (NULL)");
+    const uint64_t* io = r->in_offsets;
+    for (uint32_t i = 0; i < n; ++i)
+        if (io[i + 1] < io[i]) return perr(ENET_EINVAL, "pipeline group: offsets must be non-decreasing");
+    const uint32_t D = (uint32_t)g->pipes.size();
+    const uint64_t total = io[n] - io[0];
+    // range d = [lo[d], lo[d + 1]): lo[d] = first record starting at or after d * total / D bytes
+    std::vector<uint32_t> lo(D + 1);
+    lo[0] = 0;
+    lo[D] = n;
+    for (uint32_t d = 1; d < D; ++d) {
+        const uint64_t target = io[0] + (total * d) / D;
+        lo[d] = (uint32_t)(std::lower_bound(io, io + n, target) - io);
+        lo[d] = std::max(lo[d], lo[d - 1]);
+    }
+    std::vector<int> rc(D, ENET_OK);
+    std::vector<std::string> err(D);
+    std::vector<std::thread> th;
+    th.reserve(D);
+    for (uint32_t d = 0; d < D; ++d) {
+        const uint32_t a = lo[d], b = lo[d + 1];
+        if (a == b) continue;
+        enet_records q = *r;
+        q.count = b - a;
+        q.in_offsets = r->in_offsets + a;
+        q.out_offsets = r->out_offsets + a;
+        if (r->keys) q.keys = r->keys + (size_t)r->key_stride * a;
+        if (r->nonces) q.nonces = r->nonces + 12ull * a;
+        q.total_bytes_hint = io[b] - io[a];
+        th.emplace_back([=, &rc, &err] {
+            rc[d] = run(g->pipes[d], op, &q, counters ? counters + a : nullptr,
+                        tags_in ? tags_in + 16ull * a : nullptr, macs_in ? macs_in + 32ull * a : nullptr,
+                        tags_out ? tags_out + 16ull * a : nullptr,
+                        macs_out ? macs_out + 32ull * a : nullptr, ok_out ? ok_out + a : nullptr);
+            if (rc[d] != ENET_OK) err[d] = enet_last_error();
+        });
+    }
+    for (std::thread& t : th) t.join();
+    for (uint32_t d = 0; d < D; ++d)
+        if (rc[d] != ENET_OK) return perr(rc[d], "pipeline group, range " + std::to_string(d) + ": " + err[d]);
+    return ENET_OK;
+}
+
+}  // namespace
+
 extern "C" {
+
+enet_pipeline_group* enet_pipeline_group_create(const int* devices, uint32_t ndev,
+                                                uint64_t chunk_bytes, uint32_t streams) {
+    std::vector<int> devs;
+    if (devices && ndev) {
+        devs.assign(devices, devices + ndev);
+    } else {
+        int count = 0;
+        if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+            enet::set_last_error("enet_pipeline_group_create: no devices");
+            return nullptr;
+        }
+        for (int d = 0; d < count; ++d) devs.push_back(d);
+    }
+    auto* g = new enet_pipeline_group;
+    for (int d : devs) {
+        enet_pipeline* p = enet_pipeline_create(d, chunk_bytes, streams);
+        if (!p) {
+            const std::string e = enet_last_error();
+            enet_pipeline_group_destroy(g);
+            enet::set_last_error("enet_pipeline_group_create: device " + std::to_string(d) + ": " + e);
+            return nullptr;
+        }
+        g->pipes.push_back(p);
+    }
+    return g;
+}
+
+void enet_pipeline_group_destroy(enet_pipeline_group* g) {
+    if (!g) return;
+    for (enet_pipeline* p : g->pipes) enet_pipeline_destroy(p);
+    delete g;
+}
+
+uint32_t enet_pipeline_group_size(const enet_pipeline_group* g) {
+    return g ? (uint32_t)g->pipes.size() : 0u;
+}
+
+int enet_pipeline_group_chacha20_xor(enet_pipeline_group* g, const enet_records* r,
+                                     const uint32_t* counters) {
+    return group_run(g, Op::Xor, r, counters, nullptr, nullptr, nullptr, nullptr, nullptr);
+}
+
+int enet_pipeline_group_aead_seal(enet_pipeline_group* g, const enet_records* r, uint8_t* tags) {
+    return group_run(g, Op::Seal, r, nullptr, nullptr, nullptr, tags, nullptr, nullptr);
+}
+
+int enet_pipeline_group_aead_open(enet_pipeline_group* g, const enet_records* r,
+                                  const uint8_t* tags, uint8_t* ok) {
+    return group_run(g, Op::Open, r, nullptr, tags, nullptr, nullptr, nullptr, ok);
+}
+
+int enet_pipeline_group_aead_hmac_seal(enet_pipeline_group* g, const enet_records* r,
+                                       uint8_t* tags, uint8_t* macs) {
+    return group_run(g, Op::HmacSeal, r, nullptr, nullptr, nullptr, tags, macs, nullptr);
+}
+
+int enet_pipeline_group_aead_hmac_open(enet_pipeline_group* g, const enet_records* r,
+                                       const uint8_t* tags, const uint8_t* macs, uint8_t* ok) {
+    return group_run(g, Op::HmacOpen, r, nullptr, tags, macs, nullptr, nullptr, ok);
+}
 
 enet_pipeline* enet_pipeline_create(int device, uint64_t chunk_bytes, uint32_t streams) {
     int count = 0;

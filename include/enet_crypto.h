@@ -215,6 +215,32 @@ ENET_API int enet_pipeline_aead_hmac_seal(enet_pipeline* pipe, const enet_record
                                           uint8_t* tags, uint8_t* macs);
 ENET_API int enet_pipeline_aead_hmac_open(enet_pipeline* pipe, const enet_records* host_records,
                                           const uint8_t* tags, const uint8_t* macs, uint8_t* ok);
+/* ---- several devices of one node (no reference counterpart -- the reference
+ *      runs src/crypto on one core per call): one pipeline, host thread and stream set per device,
+ *      each call cuts the batch into contiguous record ranges balanced by input bytes and runs
+ *      them concurrently, no collective.  devices == NULL or ndev == 0: every visible device (a
+ *      device may be listed twice: two pipelines on it).  Same arguments and results as the
+ *      single-device calls above; the first failing range's status is returned. */
+typedef struct enet_pipeline_group enet_pipeline_group;
+ENET_API enet_pipeline_group* enet_pipeline_group_create(const int* devices, uint32_t ndev,
+                                                         uint64_t chunk_bytes, uint32_t streams);
+ENET_API void enet_pipeline_group_destroy(enet_pipeline_group* group);
+ENET_API uint32_t enet_pipeline_group_size(const enet_pipeline_group* group);
+ENET_API int enet_pipeline_group_chacha20_xor(enet_pipeline_group* group,
+                                              const enet_records* host_records,
+                                              const uint32_t* counters);
+ENET_API int enet_pipeline_group_aead_seal(enet_pipeline_group* group,
+                                           const enet_records* host_records, uint8_t* tags);
+ENET_API int enet_pipeline_group_aead_open(enet_pipeline_group* group,
+                                           const enet_records* host_records, const uint8_t* tags,
+                                           uint8_t* ok);
+ENET_API int enet_pipeline_group_aead_hmac_seal(enet_pipeline_group* group,
+                                                const enet_records* host_records, uint8_t* tags,
+                                                uint8_t* macs);
+ENET_API int enet_pipeline_group_aead_hmac_open(enet_pipeline_group* group,
+                                                const enet_records* host_records,
+                                                const uint8_t* tags, const uint8_t* macs,
+                                                uint8_t* ok);
 /* Pinned host memory for socket / relay buffer pools (hipHostMalloc); NULL on failure. */
 ENET_API void* enet_host_alloc(uint64_t bytes);
 ENET_API void enet_host_free(void* p);

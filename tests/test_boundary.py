@@ -118,6 +118,12 @@ def test_invalid_arguments_rejected_without_gpu(built):
     assert L.enet_pow_check_batch(3, buf, None, buf, buf, buf, None) == -1
     assert L.enet_session_key_batch(3, None, buf, buf, buf, None) == -1
     assert L.enet_pow_search_batch(0, None, None, None, 0, 10, None, None, None, None) == 0
+    # multi-device pipeline group: NULL group / descriptor rejected, size of NULL is 0
+    assert L.enet_pipeline_group_size(None) == 0
+    assert L.enet_pipeline_group_aead_seal(None, C.byref(r), buf) == -1
+    g_bad = (C.c_int * 1)(-1)
+    assert L.enet_pipeline_group_create(g_bad, 1, 0, 0) is None  # no such device
+    assert b"enet_pipeline_group_create" in L.enet_last_error()
 
 
 def test_product_never_imports_oracle():

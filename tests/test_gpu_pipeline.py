@@ -147,3 +147,49 @@ def test_pipeline_shared_key_and_errors(enet):
                          order=torch.zeros(n, dtype=torch.int32))
         with pytest.raises(enet.EnetError):
             pipe.aead_seal(bad, ct, tags)
+
+
+@pytest.mark.parametrize("devices", [[0, 0, 0], [0], None])
+def test_pipeline_group_vs_single(enet, devices):
+    """enet_pipeline_group_*: a mixed 512 B - 64 KiB batch (C5 shape) cut into byte-balanced
+    ranges over several pipelines (here three on device 0, so the split, the per-range offsets and
+    the concurrent host threads are exercised on a one-GPU box) gives exactly the bytes, tags, MACs
+    and verdicts of the single-device pipeline and of the oracle; a tampered tag and a tampered MAC
+    in different ranges are both rejected."""
+    import torch
+    n = 211
+    rng = np.random.default_rng(5)
+    lens = np.exp(rng.uniform(np.log(512), np.log(65536), n)).astype(int).tolist()
+    items = [splitmix_bytes(9000 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(9500 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(9800 + i, 12) for i in range(n)]
+    b = host_batch(enet, items, keys, nonces, True)
+    outs = []
+    for mk in (lambda: enet.PipelineGroup(devices, 1 << 20, 2), lambda: enet.Pipeline(0, 1 << 20, 2)):
+        ct = empty_like(b.arena, True)
+        tags = torch.zeros(16 * n, dtype=torch.uint8).pin_memory()
+        macs = torch.zeros(32 * n, dtype=torch.uint8).pin_memory()
+        with mk() as pipe:
+            if isinstance(pipe, enet.PipelineGroup):
+                assert pipe.size == (len(devices) if devices else torch.cuda.device_count())
+            pipe.aead_hmac_seal(b, ct, tags, macs)
+            tg, mg = tags.clone(), macs.clone()
+            tg[16 * 3] ^= 1          # first range
+            mg[32 * (n - 2) + 5] ^= 1  # last range
+            b2 = enet.Batch(ct, b.offsets, b.keys, b.nonces, total_bytes_hint=b.total_bytes_hint,
+                            max_len_hint=b.max_len_hint)
+            back = empty_like(b.arena, True)
+            ok = torch.zeros(n, dtype=torch.uint8).pin_memory()
+            pipe.aead_hmac_open(b2, back, tg, mg, ok)
+        outs.append((ct.numpy().tobytes(), tags.numpy().tobytes(), macs.numpy().tobytes(),
+                     back.numpy().tobytes(), ok.tolist()))
+    assert outs[0] == outs[1]
+    ctb, th, mh, bk, okh = outs[0]
+    got, back = records(torch.frombuffer(bytearray(ctb), dtype=torch.uint8), b.offsets), \
+        records(torch.frombuffer(bytearray(bk), dtype=torch.uint8), b.offsets)
+    for i in list(range(0, n, 13)) + [3, n - 2, n - 1]:
+        c, t = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == c and th[16 * i:16 * i + 16] == t, i
+        assert mh[32 * i:32 * i + 32] == oracle.hmac_sha256(keys[i], items[i]), i
+    for i in range(n):
+        assert (okh[i], back[i]) == ((0, bytes(lens[i])) if i in (3, n - 2) else (1, items[i])), i
