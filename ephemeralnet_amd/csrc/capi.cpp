@@ -88,6 +88,22 @@ enet::RecParams rec_params(const enet_records* r) {
         return (e && e[0] == '1') ? 1 : 0;
     }();
     if (dflt && lines_lock) p.coop_lines = 2;
+    static const int strm = [] {
+        const char* e = std::getenv("ENET_STREAM");
+        return (e && e[0] == '0') ? 0 : 1;
+    }();
+    p.stream = dflt ? strm : 0;
+    static const int dbg = [] {
+        const char* e = std::getenv("ENET_STREAM_DBG");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    p.dbg = dbg;
+    static const int var = [] {
+        const char* e = std::getenv("ENET_STREAM_VAR");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    p.var = var;
+
     if (p.coop == 4) p.coop = 1;
     // COOP 3 addresses the arena with 32-bit offsets
     if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;

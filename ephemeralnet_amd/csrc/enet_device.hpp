@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "chacha_lockstep_asm.hpp"
+
 namespace enet {
 
 // ----------------------------------------------------------------------------- ChaCha20
@@ -173,6 +175,44 @@ __device__ __forceinline__ void chacha_half_lockstep(uint32_t x[32]) {
     }
 }
 
+// The same half-round with each step (8 adds, 8 xors, 8 rotates, s_barrier) as ONE asm
+// statement whose operands are all 32 state words (chacha_lockstep_asm.hpp, generated by
+// tools/gen/gen_lockstep.py).  Single-instruction statements also get an s_nop 0 from the
+// compiler's inline-asm hazard check at every add / xor / rotate group boundary, and statements
+// naming only the words they touch make the register allocator shuffle words between VGPRs
+// (~15 v_mov per step) once the rounds are a loop; with all 32 words tied there is neither.
+// sh(base + k) runs after step k (k = 0..3), pinned there by compiler memory barriers.
+struct NoStepHook {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+template <bool DIAG, class SH = NoStepHook>
+__device__ __forceinline__ void chacha_half_lockstep2(uint32_t x[32], SH&& sh = SH{}, int base = 0) {
+    auto after = [&](int k) {
+        asm volatile("" ::: "memory");
+        sh(base + k);
+        asm volatile("" ::: "memory");
+    };
+    if constexpr (DIAG) {
+        asm volatile(ENET_LS_D0 ENET_LS_X32(x));
+        after(0);
+        asm volatile(ENET_LS_D1 ENET_LS_X32(x));
+        after(1);
+        asm volatile(ENET_LS_D2 ENET_LS_X32(x));
+        after(2);
+        asm volatile(ENET_LS_D3 ENET_LS_X32(x));
+        after(3);
+    } else {
+        asm volatile(ENET_LS_C0 ENET_LS_X32(x));
+        after(0);
+        asm volatile(ENET_LS_C1 ENET_LS_X32(x));
+        after(1);
+        asm volatile(ENET_LS_C2 ENET_LS_X32(x));
+        after(2);
+        asm volatile(ENET_LS_C3 ENET_LS_X32(x));
+        after(3);
+    }
+}
+
 __device__ __forceinline__ void chacha_block2_lockstep(const ChachaRecord& R, uint32_t ca, uint32_t cb,
                                                        uint32_t xa[16], uint32_t xb[16]) {
     uint32_t a0 = kSigma0, a4 = R.k[0], a8 = R.k[4], a12 = ca;
@@ -190,11 +230,11 @@ __device__ __forceinline__ void chacha_block2_lockstep(const ChachaRecord& R, ui
             x[16 + c + 4 * r] = R.pre[4 * (c - 1) + r];
         }
     }
-    chacha_half_lockstep<true>(x);
+    chacha_half_lockstep2<true>(x);
 #pragma unroll
     for (int i = 1; i < 10; ++i) {
-        chacha_half_lockstep<false>(x);
-        chacha_half_lockstep<true>(x);
+        chacha_half_lockstep2<false>(x);
+        chacha_half_lockstep2<true>(x);
     }
     const uint32_t ff[16] = {kSigma0, kSigma1, kSigma2, kSigma3, R.k[0], R.k[1], R.k[2], R.k[3],
                              R.k[4], R.k[5], R.k[6], R.k[7], 0u, R.n[0], R.n[1], R.n[2]};

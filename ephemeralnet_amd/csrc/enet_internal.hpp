@@ -42,6 +42,11 @@ struct RecParams {
     int coop_lines;
     int nt_stores;  // non-temporal whole-line output stores (ENET_NT_STORES=0 disables)
     int lockstep;   // staging 1: lockstep keystream in 512-thread workgroups (ENET_LOCKSTEP=0 disables)
+    int stream;     // uniform batches with L % (128 P) == 0: the streaming kernel (stream.hip;
+                    // ENET_STREAM=0 disables)
+    int dbg;        // streaming kernel timing probes (ENET_STREAM_DBG bitmask, tools only; wrong
+                    // output): 1 no HBM traffic, 4 no Poly1305, 16 no stage wait, 256 clock stamps
+    int var;        // streaming kernel code variant (ENET_STREAM_VAR, tuning)
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the
@@ -51,6 +56,9 @@ struct RecParams {
 
 // lanes: 1, 2, 4, 8 or 16 lanes per record.
 hipError_t launch_records(int mode, const RecParams& p, uint32_t lanes, hipStream_t s);
+// The streaming kernel (stream.hip): whole 512-thread workgroups of a uniform batch.
+bool stream_eligible(const RecParams& p, uint32_t lanes);
+hipError_t launch_stream(int mode, const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s);
 
 struct ShaParams {
     uint32_t n;
