@@ -572,6 +572,12 @@ def main():
     okh = int(ok.sum().item()) if args.mode != "xor" else n
     if okh != n:
         raise SystemExit(f"rank {rank}: {n - okh} records failed to open")
+    # the round trip must give the plaintext back, byte for byte (a keystream bug shared by seal
+    # and open would still verify every tag), and the ciphertext must differ from it
+    if not torch.equal(back, pt):
+        raise SystemExit(f"rank {rank}: open(seal(x)) != x")
+    if args.mode in ("aead", "xor", "store") and torch.equal(ct, pt):
+        raise SystemExit(f"rank {rank}: ciphertext equals plaintext")
 
     if rank == 0:
         total_bytes = n * L * args.steps * world

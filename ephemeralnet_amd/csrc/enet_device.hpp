@@ -185,32 +185,40 @@ __device__ __forceinline__ void chacha_half_lockstep(uint32_t x[32]) {
 struct NoStepHook {
     __device__ __forceinline__ void operator()(int) const {}
 };
-template <bool DIAG, class SH = NoStepHook>
+// BAR: s_barrier after every step (1), after steps 1 and 3 (2), after step 3 (4), never (0).
+template <bool DIAG, class SH = NoStepHook, int BAR = 1>
 __device__ __forceinline__ void chacha_half_lockstep2(uint32_t x[32], SH&& sh = SH{}, int base = 0) {
     auto after = [&](int k) {
         asm volatile("" ::: "memory");
         sh(base + k);
         asm volatile("" ::: "memory");
     };
+    constexpr bool b0 = BAR == 1, b1 = BAR == 1 || BAR == 2, b2 = BAR == 1, b3 = BAR != 0;
+#define ENET_LS_STEP(NAME, B)                               \
+    do {                                                    \
+        if constexpr (B) asm volatile(NAME ENET_LS_X32(x)); \
+        else asm volatile(NAME##_NB ENET_LS_X32(x));        \
+    } while (0)
     if constexpr (DIAG) {
-        asm volatile(ENET_LS_D0 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_D0, b0);
         after(0);
-        asm volatile(ENET_LS_D1 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_D1, b1);
         after(1);
-        asm volatile(ENET_LS_D2 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_D2, b2);
         after(2);
-        asm volatile(ENET_LS_D3 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_D3, b3);
         after(3);
     } else {
-        asm volatile(ENET_LS_C0 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_C0, b0);
         after(0);
-        asm volatile(ENET_LS_C1 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_C1, b1);
         after(1);
-        asm volatile(ENET_LS_C2 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_C2, b2);
         after(2);
-        asm volatile(ENET_LS_C3 ENET_LS_X32(x));
+        ENET_LS_STEP(ENET_LS_C3, b3);
         after(3);
     }
+#undef ENET_LS_STEP
 }
 
 __device__ __forceinline__ void chacha_block2_lockstep(const ChachaRecord& R, uint32_t ca, uint32_t cb,

@@ -45,7 +45,8 @@ struct RecParams {
     int stream;     // uniform batches with L % (128 P) == 0: the streaming kernel (stream.hip;
                     // ENET_STREAM=0 disables)
     int dbg;        // streaming kernel timing probes (ENET_STREAM_DBG bitmask, tools only; wrong
-                    // output): 1 no HBM traffic, 4 no Poly1305, 16 no stage wait, 256 clock stamps
+                    // output): 1 no HBM traffic, 2 no keystream, 4 no Poly1305, 64 no stores,
+                    // 128 no DMA, 256 clock stamps
     int var;        // streaming kernel code variant (ENET_STREAM_VAR, tuning)
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header

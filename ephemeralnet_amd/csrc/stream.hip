@@ -1,25 +1,31 @@
 // stream.hip -- the streaming ChaCha20 / ChaCha20-Poly1305 kernel for uniform batches (gfx950).
 //
 // Shape: every record is L bytes with L a multiple of 128*P (P = lanes per record), records
-// contiguous in both arenas (C2: 65 536 x 4 KiB, C4: 64 KiB chunks).  One 512-thread workgroup
-// per CU (8 waves, two per SIMD); lane j of record g owns blocks [j*B, (j+1)*B), B = L/(64 P),
-// and moves them in stages of two blocks (128 bytes per lane, 8 KiB per wave).
+// contiguous in both arenas (C2: 65 536 x 4 KiB, C4: 64 KiB chunks).  Lane j of record g owns
+// blocks [j*B, (j+1)*B), B = L/(64 P), and moves them in stages of two blocks (128 bytes per
+// lane, 8 KiB per wave).
 //
-// What differs from the staged paths of records_body.hpp (COOP 1/5): the memory traffic is
-// spread through the keystream instead of bunched at the stage boundary.
-//   * Inputs land in LDS by DMA (global_load_lds_dwordx4, whole 128-byte lines, 8 instructions
-//     per stage), into a wave-private input slab; the next stage's 8 DMAs are issued one per
-//     keystream half-round while the current stage computes, so the HBM reads of the whole chip
-//     arrive as a steady stream rather than one burst per stage, and have most of a stage to land.
-//   * Outputs go to a separate wave-private output slab; the previous stage's 8 whole-line
-//     stores are likewise issued one per half-round (the lane-linear LDS read one half-round
-//     ahead of its store).
-//   * 2 x 64 KiB of LDS per workgroup, no prefetch registers.
-//   * The keystream is the lockstep pair schedule (enet_device.hpp): both waves of a SIMD meet
-//     at s_barrier every 24 ChaCha instructions, so their full-rate adds / xors pair up.
+// One 768-thread workgroup per CU, two kinds of waves:
+//   * 8 compute waves (two per SIMD, the records' 512 lanes) run the keystream in the lockstep
+//     pair schedule (enet_device.hpp: both waves of a SIMD meet at s_barrier after every 24
+//     ChaCha instructions, so their full-rate adds / xors pair up) and Poly1305, reading their
+//     stage from an LDS input slab and writing it to an LDS output slab.  No global memory
+//     instruction, no branch and no wait sits in their keystream.
+//   * 4 memory waves (one per SIMD) move the bytes: each serves two compute waves, issuing one
+//     instruction between two consecutive keystream barriers on a fixed schedule -- the 16 LDS
+//     DMAs (global_load_lds_dwordx4, whole 128-byte lines) of the next stage early in the stage,
+//     then the 16 whole-line non-temporal stores of the previous stage spread over it.  So every
+//     CU feeds HBM a steady stream instead of bursts at stage boundaries (which, with all CUs in
+//     phase, backed the memory system up and stalled the keystream: tools/stream_probe.sh,
+//     tools/stall_pmc.sh), and the compute waves never wait on HBM.
+// Hand-offs use the shared barriers: the stage barrier S0 (inputs landed: the memory waves wait
+// for their DMAs before it; outputs of the previous stage written: the compute waves drain
+// their LDS writes before it) and keystream barrier 0 (the compute waves have read their inputs,
+// so the slab may be refilled).  LDS: 2 x 64 KiB.
 // The LDS chunk swizzle sw(o) = ((o >> 1) & 7) ^ ((o & 1) << 2) makes the own-run ds_read_b128
 // (lane groups of 16: (sw, o & 1) distinct) and ds_write_b128 (8 contiguous lanes: sw distinct)
-// conflict-free; the lane-linear DMA landing and store reads are contiguous.
+// conflict-free (PMC SQ_LDS_BANK_CONFLICT = 0); the lane-linear DMA landing and store reads are
+// contiguous.
 //
 // A workgroup first checks that each of its records sits at in_off[0] + g*L / out_off[0] + g*L
 // (the caller's hints declared the batch uniform); if any does not, the whole workgroup runs the
@@ -31,62 +37,170 @@
 
 namespace enet {
 
-constexpr uint32_t kStreamWG = 512;
+constexpr uint32_t kStreamLanes = 512;    // record lanes per workgroup (8 compute waves)
+constexpr uint32_t kStreamWG = 768;       // + 4 memory waves
+constexpr int kStreamSteps = 76;          // keystream barriers per stage (19 lockstep half-rounds)
+// Memory-wave schedule, in keystream barrier positions (an op at position k runs between barriers
+// k-1 and k; a step is ~276 shader cycles of compute, a 1 KiB DMA or store costs its memory
+// wave ~100-140 cycles to issue, so no position carries more than one of them -- two pushed
+// every fourth step to ~660 cycles, holding all 12 waves at the barrier: tools/stream_probe.py
+// trace): DMA d (0..15) at position dA + dE d, store s (0..15) at sA + sE s.
+struct StreamSched {
+    int dA, dE, sA, sE;
+};
+// 0 (default): DMA 1 + 3d, store 2 + 3s; tuning variants (ENET_STREAM_VAR, C2 shape) 1: 1 + 2d /
+// 2 + 2s, 2: 1 + 4d / 3 + 4s, 3: 1 + d / 18 + 3s.  Measured (C2 seal, us): 132 / 135 / 134 / 138.
+__device__ constexpr StreamSched stream_sched(int v) {
+    return v == 1 ? StreamSched{1, 2, 2, 2} : v == 2 ? StreamSched{1, 4, 3, 4}
+         : v == 3 ? StreamSched{1, 1, 18, 3} : StreamSched{1, 3, 2, 3};
+}
 
 __device__ __forceinline__ uint32_t stream_sw(uint32_t o) { return ((o >> 1) & 7u) ^ ((o & 1u) << 2); }
 
-template <int LOGP, int MODE, int VAR = 0>
+__device__ __forceinline__ void stream_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int LOGP, int MODE, int SCHED = 0>
 __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
+    constexpr StreamSched SC = stream_sched(SCHED);
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[kStreamWG * kRun];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[kStreamWG * kRun];
+    // input slab (DMA landing, read by the compute waves) and output slab (written by the compute
+    // waves, stored by the memory waves); wave w's part is 8 KiB at 8 KiB w
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kStreamLanes * kRun];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[kStreamLanes * kRun];
 
     const uint32_t L = (uint32_t)p.uniform_len;
-    const uint32_t gid = blockIdx.x * kStreamWG + threadIdx.x;
+    const bool compute = threadIdx.x < kStreamLanes;
+    const uint32_t gid = blockIdx.x * kStreamLanes + (compute ? threadIdx.x : 0u);
     const uint32_t rec = gid >> LOGP;  // the launch covers records [0, n), n = whole workgroups
     const uint32_t j = gid & (P - 1);
     const uint64_t i0 = p.in_off[0], o0 = p.out_off[0];
     {
-        const bool mine = p.in_off[rec] == i0 + (uint64_t)rec * L &&
-                          p.in_off[rec + 1] == i0 + (uint64_t)(rec + 1) * L &&
-                          p.out_off[rec] == o0 + (uint64_t)rec * L &&
-                          p.out_off[rec + 1] == o0 + (uint64_t)(rec + 1) * L;
+        const bool mine = !compute || (p.in_off[rec] == i0 + (uint64_t)rec * L &&
+                                       p.in_off[rec + 1] == i0 + (uint64_t)(rec + 1) * L &&
+                                       p.out_off[rec] == o0 + (uint64_t)rec * L &&
+                                       p.out_off[rec + 1] == o0 + (uint64_t)(rec + 1) * L);
         if (!__syncthreads_and(mine ? 1 : 0)) {
-            records_body<LOGP, MODE, FR_NONE, 7>(p);
+            if (compute) records_body<LOGP, MODE, FR_NONE, 7>(p);
             return;
         }
     }
 
     const uint32_t lane = threadIdx.x & 63u;
-    // scalar: the slot tests in the keystream stay SALU branches
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t B = L >> (6 + LOGP);  // blocks per lane (the host launches L % (128 P) == 0)
     const uint32_t S = B >> 1;           // stages
-    const uint32_t kk = lane & 7u;
-    const uint32_t wgid0 = blockIdx.x * kStreamWG + (wave << 6);
-    // load / store roles: instruction i moves 16-byte chunk kk ^ sw(o) of owner o = 8i + lane/8
-    // of the wave.  Its arena offset is off(i) = off(i & 1) + (i >> 1) * (16 / P) * L (owner o's
-    // record advances by 8/P per instruction for P <= 8 and by 1 per two for P = 16, its lane
-    // within the record and sw(o) ^ sw(o mod 16) only alternate).  32-bit offsets from the arena
-    // bases: the host launches this kernel only for arenas < 4 GiB.
-    uint32_t off01[2];
+    const int dbg = p.dbg;
+    const bool mem = !(dbg & 1);
+
+    if (!compute) {
+        // ================================================================ memory waves
+        // Memory wave m serves compute waves 2m and 2m+1.  Instruction i of compute wave c moves
+        // 16-byte chunk kk ^ sw(o) of its owner o = 8i + lane/8; the arena offset is
+        // off(c, i) = off(c, i & 1) + (i >> 1) * (16 / P) * L (owner o's record advances by 8/P
+        // per instruction for P <= 8 and by one per two for P = 16; its lane within the record and
+        // sw(o) ^ sw(o mod 16) only alternate).  32-bit offsets from the arena bases: the host
+        // launches this kernel only for arenas < 4 GiB.
+        const uint32_t m = wave - 8u;
+        const uint32_t kk = lane & 7u;
+        uint32_t offA[2], offAB[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const uint32_t o = 8u * i + (lane >> 3);
-        const uint32_t go = wgid0 + o;
-        off01[i] = (go >> LOGP) * L + (((go & (P - 1)) * B) << 6) + 16u * (kk ^ stream_sw(o));
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t wg0 = blockIdx.x * kStreamLanes + (2u * m + c) * 64u;
+            uint32_t o2[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t o = 8u * i + (lane >> 3);
+                const uint32_t go = wg0 + o;
+                o2[i] = (go >> LOGP) * L + (((go & (P - 1)) * B) << 6) + 16u * (kk ^ stream_sw(o));
+            }
+            offA[c] = o2[0];
+            offAB[c] = o2[1] - o2[0];
+        }
+        // every slot's lane offset precomputed (16 VGPRs): a memory wave shares its SIMD with two
+        // compute waves that keep the VALU saturated, so each VALU instruction it issues waits for
+        // a slot -- the address arithmetic of a store (~10 VALU) held it ~300 cycles past the
+        // next barrier (tools/stream_probe.py trace).  Slots are SALU + VMEM / LDS only.
+        const uint32_t offD = (16u >> LOGP) * L;
+        uint32_t offs[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            offs[s] = offA[s >> 3] + (uint32_t)(s & 1) * offAB[s >> 3] + (uint32_t)((s & 7) >> 1) * offD;
+        const uint8_t* ibase = p.in + i0;
+        uint8_t* obase = p.out + o0;
+        // this wave's parts of the slabs: compute waves 2m and 2m+1, adjacent
+        const uint32_t in_part = (uint32_t)reinterpret_cast<uintptr_t>(s_in) + 2u * m * (64u * kRun);
+        const uint8_t* out_part = s_out + 2u * m * (64u * kRun) + 16u * lane;
+        // op s (0..15) = instruction s & 7 of compute wave 2m + (s >> 3): 1 KiB group 1024 s of
+        // the part.  The DMA is issued from inline asm (M0 saved and restored in the statement):
+        // the compiler then sees no LDS DMA and puts no vmcnt wait in front of the LDS reads it
+        // cannot prove disjoint from the landing slab; the landing is awaited explicitly before
+        // the stage barrier.
+        auto dma = [&](const uint8_t* base, int s) {
+            const uint32_t m0 = in_part + 1024u * (uint32_t)s;
+            uint32_t keep;
+            asm volatile("s_mov_b32 %0, m0\n s_mov_b32 m0, %2\n s_nop 0\n global_load_lds_dwordx4 %1, %3\n s_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(offs[s]), "s"(m0), "s"(base) : "memory");
+        };
+        auto ldsread = [&](int s) {
+            return *reinterpret_cast<const uint4*>(out_part + 1024u * (uint32_t)s);
+        };
+        // whole non-temporal lines, SGPR base + VGPR offset: no VALU in the slot (a 64-bit address
+        // add waited for a VALU issue slot behind the compute waves).  From inline asm, so the
+        // store is absent from the compiler's vmcnt bookkeeping: the stage-end waits count it.
+        auto store = [&](uint8_t* base, int s, uint4 v) {
+            enet_u32x4 d = {v.x, v.y, v.z, v.w};
+            asm volatile("global_store_dwordx4 %0, %1, %2 nt\n s_nop 1"
+                         :: "v"(offs[s]), "v"(d), "s"(base) : "memory");
+        };
+        if (mem) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) dma(ibase, s);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        for (uint32_t st = 0; st < S; ++st) {
+            stream_barrier();  // S0(st): stage st landed; stage st-1's outputs in the output slab
+            const bool more = mem && st + 1 < S && !(dbg & 128), prev = mem && st > 0 && !(dbg & 64);
+            const uint8_t* inext = ibase + (size_t)kRun * (st + 1);
+            uint8_t* oprev = obase + (size_t)kRun * (st - 1);
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (__builtin_expect(prev, 1)) v = ldsread(0);
+#pragma unroll
+            for (int k = 0; k < kStreamSteps; ++k) {
+                if (k >= SC.dA && (k - SC.dA) % SC.dE == 0 && (k - SC.dA) / SC.dE < 16) {
+                    // the compute waves read their runs before barrier 0
+                    if (__builtin_expect(more, 1)) dma(inext, (k - SC.dA) / SC.dE);
+                }
+                if (k >= SC.sA && (k - SC.sA) % SC.sE == 0 && (k - SC.sA) / SC.sE < 16) {
+                    const int sl = (k - SC.sA) / SC.sE;
+                    if (__builtin_expect(prev, 1)) {
+                        store(oprev, sl, v);  // (waits for its LDS read)
+                        if (sl < 15) v = ldsread(sl + 1);
+                    }
+                }
+                stream_barrier();
+            }
+            // the next stage has landed: the stores issued after the last DMA may still be in
+            // flight (vmcnt retires in issue order)
+            constexpr int kLastDma = SC.dA + 15 * SC.dE;
+            constexpr int kStoresAfter = kLastDma < SC.sA ? 16
+                                       : (kLastDma >= SC.sA + 15 * SC.sE ? 0
+                                          : 15 - (kLastDma - SC.sA) / SC.sE);
+            if (__builtin_expect(prev, 1)) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStoresAfter) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        stream_barrier();  // F1: the last stage's outputs are in slab (S-1) & 1
+        if (S > 0 && mem) {
+            uint8_t* olast = obase + (size_t)kRun * (S - 1);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) store(olast, s, ldsread(s));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store done (tamper zeroing)
+        stream_barrier();  // F2
+        return;
     }
-    const uint32_t offD = (16u >> LOGP) * L;
-    const uint32_t offA = off01[0], offAB = off01[1] - off01[0];
-    auto off = [&](uint32_t i) { return offA + (i & 1u) * offAB + (i >> 1) * offD; };
-    const uint8_t* ibase = p.in + i0;
-    uint8_t* obase = p.out + o0;
-    const bool nt = p.nt_stores && (reinterpret_cast<uintptr_t>(obase) & 127u) == 0;
-    uint8_t* win = s_in + wave * (64u * kRun);
-    uint8_t* wout = s_out + wave * (64u * kRun);
-    uint8_t* myin = win + lane * kRun;
-    uint8_t* myout = wout + lane * kRun;
+
+    // ==================================================================== compute waves
     const uint32_t msw = stream_sw(lane);
 
     // ---- per-record ChaCha20 constants
@@ -106,29 +220,10 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         ctr = p.counters ? p.counters[(size_t)rec * (p.counter_stride ? p.counter_stride : 1u)] : 0u;
     ctr += j * B;  // this lane's first block (u32 wrap, ChaCha20.cpp:110)
 
-    // The DMA is issued from inline asm: the compiler then sees no LDS DMA, and does not put an
-    // s_waitcnt vmcnt(0) in front of every later LDS read it cannot prove disjoint from the
-    // landing slab (which would wait out each DMA right after issuing it).  The landing is
-    // awaited explicitly at the stage start; own-run reads are ordered after that wait by its
-    // memory clobber.
-    const uint32_t win_lds = (uint32_t)reinterpret_cast<uintptr_t>(win);
-    auto dma = [&](uint32_t st, uint32_t i) {
-        const uint32_t voff = off(i) + kRun * st;
-        const uint32_t m0 = __builtin_amdgcn_readfirstlane(win_lds + 1024u * i);
-        asm volatile("s_mov_b32 m0, %1\n s_nop 0\n global_load_lds_dwordx4 %0, %2"
-                     :: "v"(voff), "s"(m0), "s"(ibase) : "memory");
-    };
-
-    const int dbg = p.dbg;
     uint64_t clk0 = 0, rt0 = 0;
     if (dbg & 256) {  // clock probe: shader cycles and 100 MHz ticks around the whole body
         clk0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
-    }
-    const bool mem = !(dbg & 1);
-    if (mem) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dma(0, i);
     }
 
     // ---- Poly1305: one-time key from block 0 (runs while stage 0 lands); lane 0 absorbs the AAD
@@ -168,38 +263,17 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     const uint32_t ff[16] = {kSigma0, kSigma1, kSigma2, kSigma3, R.k[0], R.k[1], R.k[2], R.k[3],
                              R.k[4], R.k[5], R.k[6], R.k[7], 0u, R.n[0], R.n[1], R.n[2]};
     for (uint32_t st = 0; st < S; ++st) {
-        // Stage st has landed.  Each memory slot issues its DMA before its store, so from the
-        // third stage on only the last store may still be in flight (vmcnt retires in order).
-        if (mem && !(dbg & 16)) {
-            if (st >= 2) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        ENET_WAVE_LDS_SYNC();
+        // S0(st): the memory waves saw stage st land; this wave's output writes are done
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stream_barrier();
+        uint8_t* myrun = s_in + threadIdx.x * kRun;
+        // the run is read now and consumed after the keystream, so its LDS latency is hidden
         uint32_t w[32];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(myin + 16u * (k ^ msw));
+            const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
             w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
         }
-        if (MODE == MODE_OPEN && !(dbg & 4)) {
-            poly_block64(h, PR, w);
-            poly_block64(h, PR, w + 16);
-        }
-        const bool more = mem && st + 1 < S, prev = mem && st > 0;
-        uint4 pv = make_uint4(0, 0, 0, 0);
-        if (prev) pv = *reinterpret_cast<const uint4*>(wout + 16u * lane);
-        // Memory slot i (0..7) of this wave: DMA i of stage st+1, store i of stage st-1 and the
-        // lane-linear read for store i+1.  Slot i runs in double round i+1 after lockstep step
-        // `wave` (0..7), so the workgroup's waves take turns at the texture unit one step at a
-        // time instead of all eight queueing at the same barrier.
-        auto slot = [&](uint32_t i) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // own-run reads / pv done
-            if (more) dma(st + 1, i);
-            if (prev) {
-                store_stream(obase + (off(i) + kRun * (st - 1)), pv, nt);
-                if (i < 7) pv = *reinterpret_cast<const uint4*>(wout + 1024u * (i + 1) + 16u * lane);
-            }
-        };
         const uint32_t c0 = ctr + 2u * st;
         uint32_t x[32];
         {
@@ -218,30 +292,22 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
                 }
             }
         }
-        chacha_half_lockstep2<true>(x);
-        // double rounds 1..9 as a loop (not unrolled: the hot loop stays a few KiB of code)
-        auto dround = [&](uint32_t dr) {
-            const uint32_t my_step = (dr <= 8 && (more || prev)) ? wave : 99u;
-            // the slot is rare (1 step in 8): keep the common path free of taken branches -- a
-            // taken branch right after the step's s_barrier stalls both waves of the SIMD for the
-            // instruction refetch (~100 cycles measured; 72 per stage cost more than HBM did)
-            auto at = [&](int k) {
-                if (__builtin_expect((uint32_t)k == my_step, 0)) slot(dr - 1);
-            };
-            if constexpr (VAR & 2) {
+        // the input run is in registers before keystream barrier 0: the slab may be refilled
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (__builtin_expect(dbg & 2, 0)) {  // probe: no keystream, the barriers only
+#pragma unroll
+            for (int k = 0; k < kStreamSteps; ++k) stream_barrier();
+        } else {
+            chacha_half_lockstep2<true>(x);
+#pragma unroll
+            for (int dr = 1; dr < 10; ++dr) {
                 chacha_half_lockstep2<false>(x);
                 chacha_half_lockstep2<true>(x);
-            } else {
-                chacha_half_lockstep2<false>(x, at, 0);
-                chacha_half_lockstep2<true>(x, at, 4);
             }
-        };
-        if constexpr (VAR & 1) {
-#pragma unroll
-            for (uint32_t dr = 1; dr < 10; ++dr) dround(dr);
-        } else {
-#pragma unroll 1
-            for (uint32_t dr = 1; dr < 10; ++dr) dround(dr);
+        }
+        if (MODE == MODE_OPEN && !(dbg & 4)) {
+            poly_block64(h, PR, w);
+            poly_block64(h, PR, w + 16);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -252,21 +318,16 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             poly_block64(h, PR, w);
             poly_block64(h, PR, w + 16);
         }
-        // outputs into the own run of the output slab (its previous contents were read above)
+        // outputs into the own run of the output slab (the memory waves have read its previous
+        // contents out by now)
+        uint8_t* myout = s_out + threadIdx.x * kRun;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             *reinterpret_cast<uint4*>(myout + 16u * (k ^ msw)) =
                 make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
-        ENET_WAVE_LDS_SYNC();
     }
-    // the last stage's stores
-    if (S > 0 && mem) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint4 v = *reinterpret_cast<const uint4*>(wout + 1024u * i + 16u * lane);
-            store_stream(obase + (off(i) + kRun * (S - 1)), v, nt);
-        }
-    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    stream_barrier();  // F1
 
     if (dbg & 256) {  // 4 words at the workgroup's first tag slot: clk0, rt0, clk1, rt1
         const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
@@ -274,8 +335,10 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             uint64_t* d = reinterpret_cast<uint64_t*>(p.tag_out + 16ull * rec);
             d[0] = clk0; d[1] = rt0; d[2] = clk1; d[3] = rt1;
         }
+        stream_barrier();  // F2
         return;
     }
+    uint32_t diff = 0;
     if (kPoly) {
         // length block LE64(|aad|) || LE64(|ct|), owned by the last lane of the record
         const uint32_t nct = L >> 4;
@@ -307,18 +370,16 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             }
         } else {
             const uint32_t* tp = reinterpret_cast<const uint32_t*>(p.tag_in + 16ull * rec);
-            const uint32_t diff = (tag[0] ^ tp[0]) | (tag[1] ^ tp[1]) | (tag[2] ^ tp[2]) | (tag[3] ^ tp[3]);
+            diff = (tag[0] ^ tp[0]) | (tag[1] ^ tp[1]) | (tag[2] ^ tp[2]) | (tag[3] ^ tp[3]);
             if (j == 0) p.ok[rec] = diff == 0 ? 1 : 0;
-            if (diff != 0) {
-                // authentication failed: do not release plaintext.  Other lanes of this wave
-                // stored this lane's segment (owners are the wave's own lanes): let every store
-                // of the wave complete before overwriting it.
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                uint8_t* seg = obase + (uint64_t)rec * L + ((uint64_t)j * B << 6);
-                for (uint32_t c = 0; c < 4 * B; ++c)
-                    *reinterpret_cast<uint4*>(seg + 16ull * c) = make_uint4(0, 0, 0, 0);
-            }
         }
+    }
+    stream_barrier();  // F2: the memory waves' stores of this workgroup are complete
+    if (MODE == MODE_OPEN && diff != 0) {
+        // authentication failed: do not release plaintext
+        uint8_t* seg = p.out + o0 + (uint64_t)rec * L + ((uint64_t)j * B << 6);
+        for (uint32_t c = 0; c < 4 * B; ++c)
+            *reinterpret_cast<uint4*>(seg + 16ull * c) = make_uint4(0, 0, 0, 0);
     }
 }
 
@@ -326,9 +387,7 @@ template <int MODE>
 static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s) {
     switch (lanes) {
         case 1: hipLaunchKernelGGL((stream_kernel<0, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
-        case 2:
-            // tuning variants of the C2 shape (ENET_STREAM_VAR: 1 unrolled double rounds, 2 no
-            // memory slots -- timing only, 3 both)
+        case 2:  // memory schedule variants of the C2 shape (ENET_STREAM_VAR, tuning)
             switch (p.var) {
                 case 1: hipLaunchKernelGGL((stream_kernel<1, MODE, 1>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 2: hipLaunchKernelGGL((stream_kernel<1, MODE, 2>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
@@ -347,7 +406,7 @@ static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_
 bool stream_eligible(const RecParams& p, uint32_t lanes) {
     const uint64_t L = p.uniform_len;
     return p.stream && L != 0 && p.order == nullptr && L % (128ull * lanes) == 0 &&
-           L * (uint64_t)p.n <= 0xFFFFFFFFull && p.n >= kStreamWG / lanes;
+           L * (uint64_t)p.n <= 0xFFFFFFFFull && p.n >= kStreamLanes / lanes;
 }
 
 hipError_t launch_stream(int mode, const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s) {

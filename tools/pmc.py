@@ -31,8 +31,21 @@ PASSES = [
 ]
 
 
+# --passes stall: where the waves of the streaming kernel wait (issue stalls at the texture unit,
+# FIFO-full cycles, L2-to-fabric credit stalls)
+STALL_PASSES = [
+    ["SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_VMEM",
+     "SQ_INST_CYCLES_VMEM_RD", "SQ_INST_CYCLES_VMEM_WR", "SQ_ACTIVE_INST_ANY"],
+    ["SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_VMEM_TA_CMD_FIFO_FULL", "SQ_VMEM_WR_TA_DATA_FIFO_FULL",
+     "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_IFETCH", "SQ_BUSY_CYCLES",
+     "TA_ADDR_STALLED_BY_TC_CYCLES", "TA_DATA_STALLED_BY_TC_CYCLES", "GRBM_GUI_ACTIVE"],
+    ["TCC_EA0_WRREQ_STALL", "TCC_EA0_RDREQ_DRAM_CREDIT_STALL", "TCC_EA0_WRREQ_DRAM_CREDIT_STALL",
+     "GRBM_GUI_ACTIVE"],
+]
+
+
 def kernel_key(name: str):
-    if "records_kernel" not in name and "sha_kernel" not in name:
+    if "records_kernel" not in name and "sha_kernel" not in name and "stream_kernel" not in name:
         return None
     return name.split("(")[0].replace("void ", "")
 
@@ -42,13 +55,14 @@ def main():
     ap.add_argument("--out", default="gpurun_out/pmc")
     ap.add_argument("--summary", default=None)
     ap.add_argument("--config", default=None, help="JSON dict recorded as the workload config")
+    ap.add_argument("--passes", default="default", choices=["default", "stall"])
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
     os.makedirs(a.out, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
-    for i, counters in enumerate(PASSES):
+    for i, counters in enumerate(PASSES if a.passes == "default" else STALL_PASSES):
         tag = f"p{i}"
         rc = subprocess.run(["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d",
                              a.out, "-o", tag, "--", *cmd], env=env,

@@ -14,6 +14,10 @@ ap.add_argument("--records", type=int, default=65536)
 ap.add_argument("--record-bytes", type=int, default=4096)
 ap.add_argument("--mode", default="aead")
 ap.add_argument("--reps", type=int, default=200)
+ap.add_argument("--alt", action="store_true",
+                help="alternate seal(pt -> ct) and seal(ct -> back), the bench's memory pattern "
+                     "(each kernel reads what the previous one wrote; back-to-back launches of one "
+                     "kernel re-read an input the 256 MiB Infinity Cache partly holds)")
 a = ap.parse_args()
 n, L = a.records, a.record_bytes
 dev = torch.device("cuda", 0)
@@ -24,14 +28,20 @@ offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device=dev)
 ct = torch.empty_like(pt)
 tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
 b = E.Batch(pt, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+b2 = E.Batch(ct, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+back = torch.empty_like(pt)
+tags2 = torch.empty_like(tags)
 st = torch.cuda.current_stream(dev)
+flip = [0]
 
 
 def f():
+    src, dst, tg = (b, ct, tags) if not (a.alt and flip[0]) else (b2, back, tags2)
+    flip[0] ^= 1
     if a.mode == "aead":
-        E.aead_seal(b, ct, tags, stream=st)
+        E.aead_seal(src, dst, tg, stream=st)
     else:
-        E.chacha20_xor(b, ct, stream=st)
+        E.chacha20_xor(src, dst, stream=st)
 
 
 for _ in range(300):
@@ -45,7 +55,7 @@ e1.record(st)
 e1.synchronize()
 us = e0.elapsed_time(e1) / a.reps * 1e3
 dbg = int(os.environ.get("ENET_STREAM_DBG", "0"))
-out = {"dbg": dbg, "mode": a.mode, "us": round(us, 2), "GBs_alg": round(n * (2 * L + 64) / us / 1e3, 1)}
+out = {"alt": a.alt, "dbg": dbg, "mode": a.mode, "us": round(us, 2), "GBs_alg": round(n * (2 * L + 64) / us / 1e3, 1)}
 if dbg & 256 and a.mode == "aead":
     # per-workgroup stamps (stream.hip): in-kernel clock = d(memtime) / d(memrealtime) * 100 MHz
     lanes = E.lanes_per_record(n, n * L, L)
@@ -58,4 +68,15 @@ if dbg & 256 and a.mode == "aead":
     out["clock_ghz_median"] = round(float(ghz.median()), 3)
     out["clock_ghz_min"] = round(float(ghz.min()), 3)
     out["wg_us_median"] = round(float(((d[:, 3] - d[:, 1]) / 100.0).median()), 2)
+if dbg & 8192 and a.mode == "aead":
+    # memory-wave trace (stream.hip): per (workgroup, memory wave) 64 barrier-exit stamps and 16
+    # store issue times of stage 3
+    t = tags.view(torch.int32).cpu().numpy().view("u4")[: 4 * 4 * 128].reshape(16, 128).astype("int64")
+    import numpy as np
+    ex, ar = t[:, :64], t[:, 64:128]
+    own = ar[:, 1:] - ex[:, :-1]   # memory wave: previous barrier exit -> this arrival
+    wait = ex[:, 1:] - ar[:, 1:]   # memory wave: arrival -> exit (waiting for the others)
+    out["step_cycles_wg0_mw0"] = (ex[0, 1:] - ex[0, :-1]).tolist()
+    out["mw_own_cycles_wg0_mw0"] = own[0].tolist()
+    out["mw_wait_cycles_wg0_mw0"] = wait[0].tolist()
 print(json.dumps(out))
