@@ -27,9 +27,9 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 # VALU: gfx950 issues a full-rate wave64 op (v_add/v_xor/v_lshrrev/v_bitop3 ...) every 2 cycles per
 # SIMD once two waves share it, half-rate ops (v_alignbit = the ChaCha rotate, v_mad_u64_u32 =
-# the Poly1305 limb product, carries) every 4+ (tools/ubench_mix*.hip).  The binding ceiling of
-# this kernel is therefore its own instruction mix: the compute-only rate of the same stage body
-# with no memory traffic (tools/ubench_seal.hip), committed in VALU_CEILING_FILE.
+# the Poly1305 limb product, carries) every 4+ (tools/ubench_mix*.hip).  valu_roofline reports the
+# ISA bound of the instruction mix (48.3 G blocks/s for seal/open) and, beside it, the measured
+# compute-only rate of the kernel itself (memory waves idle), both in VALU_CEILING_FILE.
 VALU_ISSUE_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, full-rate ops only
 WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
@@ -42,8 +42,8 @@ METRICS = {  # the headline is `aead`; the others are SURVEY 8d/8f side measurem
     "wire": "GiB/s session wire frames seal+open (device-resident)",
     "store": "GiB/s chunk store+fetch pipeline, SHA-256 + ChaCha20 (device-resident)",
 }
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r01.json")
-VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "valu_ceiling_r01.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r02.json")
+VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "valu_ceiling_r02.json")
 
 
 def parse():
@@ -556,19 +556,24 @@ def main():
 
     # per-kernel durations: HIP events on the launch stream bracketing back-to-back launches of
     # one kernel (separate from the timed region so the markers do not add kernel gaps there)
-    def kernel_ms(fn, reps):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            fn()
-        e1.record(stream)
-        e1.synchronize()
-        return e0.elapsed_time(e1) / reps
+    # Timed in the same seal/open alternation as the timed region: each kernel reads what the
+    # other just wrote.  (Back-to-back launches of one kernel re-read an input that the 256 MiB
+    # Infinity Cache partly still holds, and read 4-6 % fast at C2.)
+    def kernel_ms_alt(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps + 1)]
+        ev[0].record(stream)
+        for i in range(reps):
+            seal()
+            ev[2 * i + 1].record(stream)
+            open_()
+            ev[2 * i + 2].record(stream)
+        ev[-1].synchronize()
+        s_ms = sum(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps)) / reps
+        o_ms = sum(ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(reps)) / reps
+        return s_ms, o_ms
 
     reps = max(4, args.steps)
-    seal_ms = kernel_ms(seal, reps)
-    open_ms = kernel_ms(open_, reps)
+    seal_ms, open_ms = kernel_ms_alt(reps)
     okh = int(ok.sum().item()) if args.mode != "xor" else n
     if okh != n:
         raise SystemExit(f"rank {rank}: {n - okh} records failed to open")
@@ -599,10 +604,9 @@ def main():
         if args.mode in ("aead", "xor") and os.path.exists(VALU_CEILING_FILE):
             with open(VALU_CEILING_FILE) as f:
                 ceil = json.load(f)
-            # the kernel runs the lockstep keystream by default: its compute-only rate is the ceiling
-            key = "seal_open_stage" if args.mode == "aead" else "xor_stage"
-            lk = key + "_lockstep_Gblocks_per_s"
-            peak = ceil[lk if lk in ceil else key + "_Gblocks_per_s"]["2_waves_per_simd"]
+            key = "seal_open_Gblocks_per_s" if args.mode == "aead" else "xor_Gblocks_per_s"
+            peak = ceil["isa_bound"][key]
+            comp = ceil["compute_only"][key]
             achieved = blocks / dom_s / 1e9
             valu = {
                 "achieved": round(achieved, 2),
@@ -610,8 +614,12 @@ def main():
                 "unit": "G ChaCha20 blocks/s (64 B) incl. Poly1305" if args.mode == "aead"
                         else "G ChaCha20 blocks/s (64 B)",
                 "frac": round(achieved / peak, 4),
-                "peak_is": "compute-only rate of the same (lockstep) stage body, no memory "
-                           "(tools/ubench_seal.hip; " + os.path.relpath(VALU_CEILING_FILE, ROOT) + ")",
+                "peak_is": "ISA bound of the instruction mix at 2.4 GHz, two waves per SIMD "
+                           "(" + os.path.relpath(VALU_CEILING_FILE, ROOT) + " isa_bound)",
+                "compute_only": comp,
+                "frac_of_compute_only": round(achieved / comp, 4),
+                "compute_only_is": "the same kernel with its memory waves idle "
+                                   "(ENET_STREAM_DBG=257, " + os.path.relpath(VALU_CEILING_FILE, ROOT) + ")",
             }
         if os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
@@ -620,7 +628,8 @@ def main():
             lg, md = lanes.bit_length() - 1, 1 if dom == "seal" else 2
             # the lockstep kernel (default for 64-byte-multiple records), else the 256-thread one
             k = None
-            for want in (f"records_kernel_l<{lg}, {md}, 5>", f"records_kernel<{lg}, {md}, 0, 1>"):
+            for want in (f"stream_kernel<{lg}, {md}, 0>", f"records_kernel_l<{lg}, {md}, 5>",
+                         f"records_kernel<{lg}, {md}, 0, 1>"):
                 k = k or next((v for name, v in pmc.get("kernels", {}).items() if want in name), None)
             if k and args.mode == "aead" and pmc.get("config") == {"records": n, "record_bytes": L}:
                 traffic = k.get("hbm_bytes_per_launch")
@@ -665,7 +674,7 @@ def main():
             "open_gibs": round(n * L / (open_ms * 1e-3) / 2**30, 1),
             "roofline": {
                 "bound": "hbm",
-                "kernel": (f"records_kernel ({dom})" if args.mode in ("aead", "xor")
+                "kernel": (f"stream_kernel ({dom})" if args.mode in ("aead", "xor")
                            else f"{args.mode} {dom} kernel sequence"),
                 "achieved": round(dom_gbs, 1),
                 "peak": HBM_PEAK_GBS,
@@ -674,7 +683,8 @@ def main():
                 "traffic": traffic,
                 "traffic_source": pmc_note,
                 "algorithmic_bytes_per_launch": seal_bytes if dom == "seal" else open_bytes,
-                "note": "int32 VALU-issue-bound, not HBM-bound: see valu_roofline",
+                "note": "VALU-bound (ChaCha20 ARX + Poly1305 limb products) with HBM traffic of the "
+                        "same order: see valu_roofline",
             },
             "valu_roofline": valu,
         }

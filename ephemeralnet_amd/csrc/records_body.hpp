@@ -70,8 +70,8 @@ __device__ __forceinline__ void poly_block64(uint32_t h[5], const PolyR32& R, co
 // in_off[0] + g*L): whole-block stages of kStage blocks per lane are moved wave-cooperatively.
 // Load instruction i of a stage serves owners 8i..8i+7 of the wave (64 lanes x 16 B = 8 owners x
 // 128 contiguous bytes = whole 128-byte lines), lands in a wave-private LDS slab
-// [owner][128 B] whose 16-byte chunks are XOR-swizzled by (owner >> 1) & 7 (conflict-free
-// ds_read_b128), and each lane then reads its own two blocks.  Outputs take the reverse trip.
+// [owner][128 B] whose 16-byte chunks are XOR-swizzled by slab_sw(owner) (conflict-free
+// ds_read_b128 and ds_write_b128), and each lane then reads its own two blocks.  Outputs take the reverse trip.
 // Within one wave, DS instructions execute in issue order, so handing LDS data between lanes
 // of the same wave needs only a compiler barrier -- a wavefront-scope fence would also drain the
 // in-flight global loads/stores (s_waitcnt vmcnt(0)) and serialise every stage.
@@ -87,6 +87,15 @@ __device__ __forceinline__ void poly_block64(uint32_t h[5], const PolyR32& R, co
     asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), \
                       "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]), "+v"(a[11]), \
                       "+v"(a[12]), "+v"(a[13]), "+v"(a[14]), "+v"(a[15])::"memory")
+
+// 16-byte chunk c of owner o's run sits at 128 o + 16 (c ^ slab_sw(o)) in a staging slab.  The
+// own-run ds_read_b128 serves lanes in groups of 16 ({0-3,12-15,20-27}, ...; bank = dword address
+// mod 64) and needs (slab_sw(o), o & 1) distinct inside each group; the own-run ds_write_b128
+// serves 8 contiguous lanes (bank = dword address mod 32) and needs slab_sw(o) distinct across
+// them.  ((o >> 1) & 7) alone met the first only: every own-run write was a 2-way conflict
+// (PMC SQ_LDS_BANK_CONFLICT 2.1 M cycles per C2 launch, profiles/pmc_r01.json); flipping bit 2
+// with o & 1 meets both (0 in profiles/pmc_r02.json).
+__device__ __forceinline__ uint32_t slab_sw(uint32_t o) { return ((o >> 1) & 7u) ^ ((o & 1u) << 2); }
 
 constexpr uint32_t kStage = 2;                 // blocks per lane per cooperative stage
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
@@ -258,7 +267,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             const uint32_t o = 8u * i + (lane >> 3);
             const uint32_t og = (wgid0 + o) >> LOGP;
             const uint32_t oj = (wgid0 + o) & (P - 1);
-            const uint32_t sw = (o >> 1) & 7u;
+            const uint32_t sw = slab_sw(o);
             // the host launches COOP only over whole waves of live records
             off[i] = (uint64_t)og * Lu + 64ull * oj * B + 16u * (kk ^ sw);
         }
@@ -269,7 +278,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
                                  (reinterpret_cast<uintptr_t>(obase) & 63u) == 0;
         uint8_t* wslab = slab + wbase * kRun;
         uint8_t* myrun = slab + threadIdx.x * kRun;
-        const uint32_t msw = (lane >> 1) & 7u;
+        const uint32_t msw = slab_sw(lane);
         // prefetch registers as plain words (a uint4 array is copied with memcpy and stays
         // in scratch)
         uint32_t pf[32];
@@ -360,7 +369,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const uint32_t o = 8u * i + (lane >> 3);
-                const uint32_t gc = kk ^ ((o >> 1) & 7u);
+                const uint32_t gc = kk ^ slab_sw(o);
                 const uint64_t run = (uint64_t)((wgid0 + o) >> LOGP) * Lu + adv;
                 if (gc < nch) {
                     const uint32_t at = gc < rem16 ? 16u * gc : rem - 16u;
@@ -444,7 +453,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const uint32_t o = 8u * i + (lane >> 3);
-                const uint32_t gc = kk ^ ((o >> 1) & 7u);
+                const uint32_t gc = kk ^ slab_sw(o);
                 const uint64_t run = (uint64_t)((wgid0 + o) >> LOGP) * Lu + adv;
                 if (gc < nch) {
                     const uint32_t at = gc < rem16 ? 16u * gc : rem - 16u;
@@ -628,6 +637,11 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         store_line(S);  // the last line when the record ends in line S (d + L > 128 S)
         cco = cend;
         ctail = cend;
+        } else {
+            // per-lane path for this workgroup: it still needs the one-time key (round 1 skipped
+            // it here, so a uniform 1500-byte batch whose in / out arenas differed mod 128 got
+            // all-zero tags; tests/test_gpu_parity.py::test_lying_hints_give_correct_bytes)
+            poly_setup();
         }
     }
     if (COOP == 3) {
@@ -654,14 +668,14 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             const uint32_t o = 8u * i + (lane >> 3);
             const uint32_t og = (wgid0 + o) >> LOGP;
             const uint32_t oj = (wgid0 + o) & (P - 1);
-            const uint32_t sw = (o >> 1) & 7u;
+            const uint32_t sw = slab_sw(o);
             off[i] = (uint32_t)((uint64_t)og * Lu + 64ull * oj * B + 16u * (kk ^ sw));
         }
         const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
         uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
         uint8_t* wslab = slab + wbase * kRun;
         uint8_t* myrun = slab + threadIdx.x * kRun;
-        const uint32_t msw = (lane >> 1) & 7u;
+        const uint32_t msw = slab_sw(lane);
         auto dma = [&](uint32_t stage) {
             const uint32_t adv = kRun * stage;
 #pragma unroll

@@ -49,19 +49,33 @@ struct StreamSched {
     int dA, dE, sA, sE;
 };
 // 0 (default): DMA 1 + 3d, store 2 + 3s; tuning variants (ENET_STREAM_VAR, C2 shape) 1: 1 + 2d /
-// 2 + 2s, 2: 1 + 4d / 3 + 4s, 3: 1 + d / 18 + 3s.  Measured (C2 seal, us): 132 / 135 / 134 / 138.
+// 2 + 2s, 2: 1 + 4d / 3 + 4s, 3: 1 + d / 18 + 3s; 4 / 5: keystream barriers every 2 / 4 steps
+// (38 / 19 positions), DMA 1 + 2d / 1 + d, store 2 + 2s / 1 + s (same position, after the DMA).
+// C2 seal kernel in the bench's alternating pattern (tools/stream_probe.py --alt), us:
+// 133 / 138 / 132 / 134 / 143 / 147 -- coarser barriers lose more lockstep pairing than they
+// give the memory waves.  Layout probes that did not help: rotating each wave's stage order
+// (arena offsets in flight differing in their low bits) 122 vs 124 us ChaCha20-only; lane j of
+// a record owning runs j, j + P, ... (P lanes read 128 P contiguous bytes per stage) 154 vs 122.
 __device__ constexpr StreamSched stream_sched(int v) {
     return v == 1 ? StreamSched{1, 2, 2, 2} : v == 2 ? StreamSched{1, 4, 3, 4}
-         : v == 3 ? StreamSched{1, 1, 18, 3} : StreamSched{1, 3, 2, 3};
+         : v == 3 ? StreamSched{1, 1, 18, 3} : v == 4 ? StreamSched{1, 2, 2, 2}
+         : v == 5 ? StreamSched{1, 1, 1, 1} : StreamSched{1, 3, 2, 3};
 }
-
-__device__ __forceinline__ uint32_t stream_sw(uint32_t o) { return ((o >> 1) & 7u) ^ ((o & 1u) << 2); }
+__device__ constexpr int stream_barf(int v) { return v == 4 ? 2 : v == 5 ? 4 : 1; }
+// stores issued at or after the last DMA's position (a store shares a position only after the DMA)
+__device__ constexpr int stream_stores_after(StreamSched sc) {
+    int n = 0;
+    for (int s = 0; s < 16; ++s) n += (sc.sA + sc.sE * s >= sc.dA + 15 * sc.dE) ? 1 : 0;
+    return n;
+}
 
 __device__ __forceinline__ void stream_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 template <int LOGP, int MODE, int SCHED = 0>
 __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     constexpr StreamSched SC = stream_sched(SCHED);
+    constexpr int BARF = stream_barf(SCHED);       // keystream steps per barrier
+    constexpr int kPos = kStreamSteps / BARF;      // barrier positions per stage
     constexpr uint32_t P = 1u << LOGP;
     constexpr bool kPoly = (MODE != MODE_XOR);
     // input slab (DMA landing, read by the compute waves) and output slab (written by the compute
@@ -112,7 +126,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             for (int i = 0; i < 2; ++i) {
                 const uint32_t o = 8u * i + (lane >> 3);
                 const uint32_t go = wg0 + o;
-                o2[i] = (go >> LOGP) * L + (((go & (P - 1)) * B) << 6) + 16u * (kk ^ stream_sw(o));
+                o2[i] = (go >> LOGP) * L + (((go & (P - 1)) * B) << 6) + 16u * (kk ^ slab_sw(o));
             }
             offA[c] = o2[0];
             offAB[c] = o2[1] - o2[0];
@@ -153,6 +167,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             asm volatile("global_store_dwordx4 %0, %1, %2 nt\n s_nop 1"
                          :: "v"(offs[s]), "v"(d), "s"(base) : "memory");
         };
+        uint64_t wait_cyc = 0;
         if (mem) {
 #pragma unroll
             for (int s = 0; s < 16; ++s) dma(ibase, s);
@@ -166,7 +181,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             uint4 v = make_uint4(0, 0, 0, 0);
             if (__builtin_expect(prev, 1)) v = ldsread(0);
 #pragma unroll
-            for (int k = 0; k < kStreamSteps; ++k) {
+            for (int k = 0; k < kPos; ++k) {
                 if (k >= SC.dA && (k - SC.dA) % SC.dE == 0 && (k - SC.dA) / SC.dE < 16) {
                     // the compute waves read their runs before barrier 0
                     if (__builtin_expect(more, 1)) dma(inext, (k - SC.dA) / SC.dE);
@@ -182,13 +197,15 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             }
             // the next stage has landed: the stores issued after the last DMA may still be in
             // flight (vmcnt retires in issue order)
-            constexpr int kLastDma = SC.dA + 15 * SC.dE;
-            constexpr int kStoresAfter = kLastDma < SC.sA ? 16
-                                       : (kLastDma >= SC.sA + 15 * SC.sE ? 0
-                                          : 15 - (kLastDma - SC.sA) / SC.sE);
+            constexpr int kStoresAfter = stream_stores_after(SC);
+            uint64_t tw0 = 0;
+            if (__builtin_expect(dbg & 2048, 0)) tw0 = __builtin_amdgcn_s_memtime();
             if (__builtin_expect(prev, 1)) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kStoresAfter) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (__builtin_expect(dbg & 2048, 0)) wait_cyc += __builtin_amdgcn_s_memtime() - tw0;
         }
+        if (__builtin_expect(dbg & 2048, 0) && lane == 0 && p.tag_out)  // probe: stage-end DMA waits
+            reinterpret_cast<uint64_t*>(p.tag_out)[blockIdx.x * 4u + m] = wait_cyc;
         stream_barrier();  // F1: the last stage's outputs are in slab (S-1) & 1
         if (S > 0 && mem) {
             uint8_t* olast = obase + (size_t)kRun * (S - 1);
@@ -201,7 +218,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     }
 
     // ==================================================================== compute waves
-    const uint32_t msw = stream_sw(lane);
+    const uint32_t msw = slab_sw(lane);
 
     // ---- per-record ChaCha20 constants
     uint32_t kw[8], nw[3];
@@ -269,10 +286,15 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         uint8_t* myrun = s_in + threadIdx.x * kRun;
         // the run is read now and consumed after the keystream, so its LDS latency is hidden
         uint32_t w[32];
+        if (__builtin_expect(dbg & 32, 0)) {  // probe: no LDS traffic in the compute waves
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
-            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            for (int k = 0; k < 32; ++k) w[k] = k * lane + st;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+            }
         }
         const uint32_t c0 = ctr + 2u * st;
         uint32_t x[32];
@@ -296,13 +318,13 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (__builtin_expect(dbg & 2, 0)) {  // probe: no keystream, the barriers only
 #pragma unroll
-            for (int k = 0; k < kStreamSteps; ++k) stream_barrier();
+            for (int k = 0; k < kPos; ++k) stream_barrier();
         } else {
-            chacha_half_lockstep2<true>(x);
+            chacha_half_lockstep2<true, NoStepHook, BARF>(x);
 #pragma unroll
             for (int dr = 1; dr < 10; ++dr) {
-                chacha_half_lockstep2<false>(x);
-                chacha_half_lockstep2<true>(x);
+                chacha_half_lockstep2<false, NoStepHook, BARF>(x);
+                chacha_half_lockstep2<true, NoStepHook, BARF>(x);
             }
         }
         if (MODE == MODE_OPEN && !(dbg & 4)) {
@@ -321,17 +343,24 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         // outputs into the own run of the output slab (the memory waves have read its previous
         // contents out by now)
         uint8_t* myout = s_out + threadIdx.x * kRun;
+        if (__builtin_expect(dbg & 32, 0)) {
+            uint32_t acc = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            *reinterpret_cast<uint4*>(myout + 16u * (k ^ msw)) =
-                make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+            for (int k = 0; k < 32; ++k) acc ^= w[k];
+            if (acc == 0x9e3779b9u) myout[0] = 1;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<uint4*>(myout + 16u * (k ^ msw)) =
+                    make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stream_barrier();  // F1
 
-    if (dbg & 256) {  // 4 words at the workgroup's first tag slot: clk0, rt0, clk1, rt1
+    if (dbg & (256 | 2048)) {  // 4 words at the workgroup's first tag slot: clk0, rt0, clk1, rt1
         const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-        if (threadIdx.x == 0 && p.tag_out) {
+        if (threadIdx.x == 0 && p.tag_out && !(dbg & 2048)) {
             uint64_t* d = reinterpret_cast<uint64_t*>(p.tag_out + 16ull * rec);
             d[0] = clk0; d[1] = rt0; d[2] = clk1; d[3] = rt1;
         }
@@ -392,6 +421,8 @@ static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_
                 case 1: hipLaunchKernelGGL((stream_kernel<1, MODE, 1>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 2: hipLaunchKernelGGL((stream_kernel<1, MODE, 2>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 3: hipLaunchKernelGGL((stream_kernel<1, MODE, 3>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
+                case 4: hipLaunchKernelGGL((stream_kernel<1, MODE, 4>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
+                case 5: hipLaunchKernelGGL((stream_kernel<1, MODE, 5>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 default: hipLaunchKernelGGL((stream_kernel<1, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
             }
             break;

@@ -1,7 +1,7 @@
 // CryptoManager.hpp -- drop-in for the reference include/ephemeralnet/crypto/CryptoManager.hpp:12-44.
 #pragma once
 
-#include "ephemeralnet/Types.hpp"
+#include "ephemeralnet/crypto/CryptoTypes.hpp"
 #include "ephemeralnet/crypto/ChaCha20.hpp"
 
 #include <optional>

@@ -13,7 +13,7 @@
 #include <utility>
 #include <vector>
 
-#include "ephemeralnet/Types.hpp"
+#include "ephemeralnet/crypto/CryptoTypes.hpp"
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 
 namespace ephemeralnet::network {

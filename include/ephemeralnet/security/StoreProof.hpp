@@ -10,7 +10,7 @@
 #include <string_view>
 #include <vector>
 
-#include "ephemeralnet/Types.hpp"
+#include "ephemeralnet/crypto/CryptoTypes.hpp"
 #include "ephemeralnet/crypto/ChaCha20.hpp"
 
 namespace ephemeralnet::security {

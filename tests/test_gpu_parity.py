@@ -608,3 +608,161 @@ def test_c1_single_key_gpu_cpu_roundtrips(enet):
     ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
     enet.aead_open(bo, back, t2, ok)
     assert int(ok.sum()) == n and torch.equal(back, b.arena)
+
+
+# ------------------------------------------------------------------------------ uniform + AAD
+@pytest.mark.parametrize("staging", [1, 3, 4, 5])
+@pytest.mark.parametrize("L,n,lanes", [(4096, 600, 2), (4096, 300, 1), (1500, 600, 1),
+                                       (65536, 40, 16), (2048, 700, 4), (640, 600, 1)])
+def test_aead_uniform_aad_vs_oracle(enet, L, n, lanes, staging):
+    """Per-record AAD of assorted lengths on the staged / streaming paths: lane 0 absorbs the AAD
+    before its run, the other lanes scale by r^e with e counting the AAD blocks.  Tags bit-exact
+    against the oracle; a tampered AAD byte is rejected and that record zeroed."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    enet.set_staging(staging)
+    alens = [[0, 1, 12, 16, 17, 100][i % 6] for i in range(n)]
+    items = [splitmix_bytes(71000 + i, L) for i in range(n)]
+    aads = [splitmix_bytes(72000 + i, a) for i, a in enumerate(alens)]
+    keys = [splitmix_bytes(73000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(74000 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces)
+    aoff = torch.tensor(np.concatenate([[0], np.cumsum(alens)]).astype(np.int64)).cuda()
+    aad = dev(b"".join(aads))
+    out = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags, aad, aoff)
+    got = records_of(host(out), b.offsets.cpu().tolist())
+    th = host(tags)
+    idx = range(n) if n * L <= 4 << 20 else np.linspace(0, n - 1, 96).astype(int)
+    for i in idx:
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i], aads[i])
+        assert got[i] == ct, (i, L)
+        assert th[16 * i:16 * i + 16] == tag, (i, L, alens[i])
+    b2 = enet.Batch(out, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    back = torch.zeros_like(out)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, back, tags, ok, aad, aoff)
+    assert int(ok.sum()) == n and torch.equal(back, b.arena)
+    bad_aad = aad.clone()
+    k = 5 if alens[5] else 4
+    bad_aad[int(aoff[k])] ^= 0x10
+    back.fill_(0xAA)
+    enet.aead_open(b2, back, tags, ok, bad_aad, aoff)
+    okh = ok.cpu().tolist()
+    assert okh[k] == 0 and sum(okh) == n - 1
+    bh = records_of(host(back), b.offsets.cpu().tolist())
+    assert bh[k] == bytes(L) and bh[k + 1] == items[k + 1]
+    enet.set_staging(-1)
+
+
+# ------------------------------------------------------------------------------ lying hints
+@pytest.mark.parametrize("staging", [1, 3, 4, 5])
+@pytest.mark.parametrize("L,lanes", [(4096, 2), (4096, 1), (1500, 1), (65536, 16), (2048, 4)])
+def test_lying_hints_give_correct_bytes(enet, L, lanes, staging):
+    """The hints say uniform (total == n * max_len_hint) but two records are 64 bytes shorter /
+    longer than max_len_hint: the staged and streaming paths address records at in_off[0] + g L,
+    so the workgroups holding them must notice and take the per-lane path.  Every record stays
+    bit-exact (seal, open, ChaCha20 xor)."""
+    import torch
+    enet.set_lanes_per_record(lanes)
+    enet.set_staging(staging)
+    n = max(600, (4 << 20) // L) if L < 65536 else 72
+    lens = [L] * n
+    lens[n // 3] -= 64
+    lens[n // 3 + 7] += 64           # total still n * L; the true maximum is L + 64
+    items = [splitmix_bytes(75000 + i, x) for i, x in enumerate(lens)]
+    keys = [splitmix_bytes(76000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(77000 + i, 12) for i in range(n)]
+    b0 = enet.make_batch(items, keys, nonces)
+    b = enet.Batch(b0.arena, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    out = out_like(b)
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    offs = b.offsets.cpu().tolist()
+    got = records_of(host(out), offs)
+    th = host(tags)
+    idx = sorted(set(list(range(0, n, max(1, n // 64))) + [n // 3 - 1, n // 3, n // 3 + 1,
+                                                            n // 3 + 7, n // 3 + 8, n - 1]))
+    for i in idx:
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct, (i, lens[i])
+        assert th[16 * i:16 * i + 16] == tag, (i, lens[i])
+    b2 = enet.Batch(out, b.offsets, b.keys, b.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    back = torch.zeros_like(out)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, back, tags, ok)
+    assert int(ok.sum()) == n and torch.equal(back, b.arena)
+    xo = out_like(b)
+    enet.chacha20_xor(b, xo)
+    xg = records_of(host(xo), offs)
+    for i in idx:
+        assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], 0), i
+    enet.set_staging(-1)
+
+
+# ------------------------------------------------------------------------------ full-size shapes
+@pytest.mark.parametrize("n,L", [(1048576, 1500), (32768, 65536)])
+def test_aead_roundtrip_full_size(enet, n, L):
+    """C3 (1 M x 1500 B: the line-staging path's 32-bit line offsets reach 1.57 GB) and the C4
+    per-GPU share (32 768 x 64 KiB, 2 GiB: the streaming kernel's 32-bit offsets) at full size:
+    open(seal(x)) == x with every tag verified, one flipped bit rejected with its record zeroed,
+    and a 512-record oracle sample bit-exact."""
+    import torch
+    enet.set_lanes_per_record(0)
+    enet.set_staging(-1)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    pt = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device="cuda", generator=g)
+    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device="cuda", generator=g)
+    nonces = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, device="cuda", generator=g)
+    offs = torch.arange(0, (n + 1) * L, L, dtype=torch.int64, device="cuda")
+    b = enet.Batch(pt, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+    ct = torch.empty_like(pt)
+    tags = torch.empty(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, ct, tags)
+    idx = np.linspace(0, n - 1, 512).astype(int)
+    rows = torch.tensor(idx, device="cuda")
+    pth = pt.view(n, L)[rows].cpu().numpy()
+    cth = ct.view(n, L)[rows].cpu().numpy()
+    kh = keys.view(n, 32)[rows].cpu().numpy()
+    nh = nonces.view(n, 12)[rows].cpu().numpy()
+    th = tags.view(n, 16)[rows].cpu().numpy()
+    for r in range(len(idx)):
+        c, t = oracle.aead_seal(kh[r].tobytes(), nh[r].tobytes(), pth[r].tobytes())
+        assert cth[r].tobytes() == c, idx[r]
+        assert th[r].tobytes() == t, idx[r]
+    victim = n - 5
+    ct[victim * L + L // 2] ^= 0x80
+    back = torch.empty_like(pt)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    b2 = enet.Batch(ct, offs, keys, nonces, total_bytes_hint=n * L, max_len_hint=L)
+    enet.aead_open(b2, back, tags, ok)
+    okh = ok.cpu()
+    assert int(okh.sum()) == n - 1 and int(okh[victim]) == 0
+    bv, pv = back.view(n, L), pt.view(n, L)
+    assert torch.equal(bv[:victim], pv[:victim]) and torch.equal(bv[victim + 1:], pv[victim + 1:])
+    assert int(bv[victim].count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("shift", [4, 64, 100])
+def test_aead_uniform_out_arena_phase(enet, shift):
+    """1500-byte uniform records whose output arena starts at another 128-byte phase than the input
+    arena: the line-staging path cannot be used and the workgroups take the per-lane path (which
+    must still derive the one-time Poly1305 key)."""
+    import torch
+    enet.set_lanes_per_record(1)
+    enet.set_staging(-1)
+    n, L = 1024, 1500
+    items = [splitmix_bytes(78000 + i, L) for i in range(n)]
+    keys = [splitmix_bytes(79000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(79500 + i, 12) for i in range(n)]
+    b = enet.make_batch(items, keys, nonces)
+    big = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    out = big[shift:shift + n * L]
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    got = records_of(host(out), b.offsets.cpu().tolist())
+    th = host(tags)
+    for i in range(0, n, 7):
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct and th[16 * i:16 * i + 16] == tag, i

@@ -79,4 +79,11 @@ if dbg & 8192 and a.mode == "aead":
     out["step_cycles_wg0_mw0"] = (ex[0, 1:] - ex[0, :-1]).tolist()
     out["mw_own_cycles_wg0_mw0"] = own[0].tolist()
     out["mw_wait_cycles_wg0_mw0"] = wait[0].tolist()
+if dbg & 2048 and a.mode == "aead":
+    import numpy as np
+    lanes = E.lanes_per_record(n, n * L, L)
+    nwg = n * lanes // 512
+    w = (tags if not a.alt else tags2).view(torch.int64).cpu().numpy()[: nwg * 4]
+    out["stage_end_dma_wait_cycles_per_wave_median"] = float(np.median(w))
+    out["stage_end_dma_wait_cycles_per_wave_max"] = float(np.max(w))
 print(json.dumps(out))
