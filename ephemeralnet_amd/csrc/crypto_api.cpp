@@ -656,6 +656,33 @@ std::vector<std::uint8_t> handshake_pow_prefix(const PeerId& initiator, const Pe
     return v;
 }
 
+namespace {
+bool node_pow_one(const std::vector<std::uint8_t>& prefix, std::uint8_t difficulty, std::uint64_t& nonce_out) {
+    if (difficulty == 0) {  // Node.cpp:213-216 / 274-277
+        nonce_out = 0;
+        return true;
+    }
+    const std::span<const std::uint8_t> ps[1] = {prefix};
+    const std::uint8_t d[1] = {difficulty};
+    const auto r = pow_search(ps, d, PowSchedule::Node, kNodePowAttempts);
+    if (!r[0].found) return false;
+    nonce_out = r[0].nonce;
+    return true;
+}
+}  // namespace
+
+bool compute_announce_pow(const ChunkId& chunk_id, const PeerId& peer_id, std::string_view endpoint,
+                          std::string_view manifest_uri, std::span<const std::uint8_t> assigned_shards,
+                          std::int64_t ttl_seconds, std::uint8_t difficulty, std::uint64_t& nonce_out) {
+    return node_pow_one(announce_pow_prefix(chunk_id, peer_id, endpoint, manifest_uri, assigned_shards, ttl_seconds),
+                        difficulty, nonce_out);
+}
+
+bool compute_handshake_pow(const PeerId& initiator, const PeerId& responder, std::uint32_t initiator_public,
+                           std::uint8_t difficulty, std::uint64_t& nonce_out) {
+    return node_pow_one(handshake_pow_prefix(initiator, responder, initiator_public), difficulty, nonce_out);
+}
+
 std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secrets,
                                                        std::span<const std::uint64_t> counters,
                                                        std::span<const std::int64_t> ticks) {

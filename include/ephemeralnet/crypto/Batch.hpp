@@ -125,6 +125,20 @@ ENET_CXX_API std::vector<std::uint8_t> announce_pow_prefix(const ChunkId& chunk_
 ENET_CXX_API std::vector<std::uint8_t> handshake_pow_prefix(const PeerId& initiator, const PeerId& responder,
                                                             std::uint32_t initiator_public);
 
+// Drop-ins for Node.cpp's file-local searches compute_announce_pow (Node.cpp:212-230) and
+// compute_handshake_pow (:269-292): same start (mt19937_64 seeded by the nonce-0 digest), same
+// attempt order and 500'000-attempt cap (Node.cpp:40,43), same nonce.  difficulty 0 -> nonce 0,
+// true.  Not found -> false and nonce_out untouched.  One device search replaces up to 500'000
+// host Sha256 constructions; a maintainer makes the Node.cpp helpers forward here.
+inline constexpr std::uint64_t kNodePowAttempts = 500'000;
+ENET_CXX_API bool compute_announce_pow(const ChunkId& chunk_id, const PeerId& peer_id, std::string_view endpoint,
+                                       std::string_view manifest_uri,
+                                       std::span<const std::uint8_t> assigned_shards, std::int64_t ttl_seconds,
+                                       std::uint8_t difficulty, std::uint64_t& nonce_out);
+ENET_CXX_API bool compute_handshake_pow(const PeerId& initiator, const PeerId& responder,
+                                        std::uint32_t initiator_public, std::uint8_t difficulty,
+                                        std::uint64_t& nonce_out);
+
 // KeyManager::derive_key (KeyManager.cpp:74-92) for many sessions:
 // HMAC-SHA256(secret_i, BE64(counter_i) || BE64(ticks_i)), ticks in ns since the steady_clock epoch
 ENET_CXX_API std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secrets,

@@ -178,8 +178,11 @@ int main() {
             auto r = crypto::batch::pow_search(ps, diff, crypto::batch::PowSchedule::Node, 500000);
             const uint64_t nn[1] = {r[0].nonce};
             auto ok = crypto::batch::pow_check(ps, nn, diff);
+            // the Node.cpp drop-in (nonce_out untouched when not found)
+            uint64_t dn = 0xFFFFFFFFFFFFFFFFull;
+            const bool df = crypto::batch::compute_handshake_pow(ia, ib, (uint32_t)std::stoul(pub), diff[0], dn);
             std::cout << (r[0].found ? 1 : 0) << " " << r[0].nonce << " " << r[0].attempts << " "
-                      << (int)ok[0] << "\n";
+                      << (int)ok[0] << " " << (df ? 1 : 0) << " " << dn << "\n";
         } else if (op == "announce_pow") {
             std::string id, peer, ep, uri, sh, ttl, d; in >> id >> peer >> ep >> uri >> sh >> ttl >> d;
             ChunkId cid{}; PeerId pid{};
@@ -192,7 +195,12 @@ int main() {
             std::span<const uint8_t> ps[1] = {pre};
             const uint8_t diff[1] = {(uint8_t)std::stoul(d)};
             auto r = crypto::batch::pow_search(ps, diff, crypto::batch::PowSchedule::Node, 500000);
-            std::cout << (r[0].found ? 1 : 0) << " " << r[0].nonce << " " << r[0].attempts << "\n";
+            uint64_t dn = 0xFFFFFFFFFFFFFFFFull;
+            const bool df = crypto::batch::compute_announce_pow(cid, pid, std::string(eb.begin(), eb.end()),
+                                                                std::string(ub.begin(), ub.end()), sb,
+                                                                std::stoll(ttl), diff[0], dn);
+            std::cout << (r[0].found ? 1 : 0) << " " << r[0].nonce << " " << r[0].attempts << " "
+                      << (df ? 1 : 0) << " " << dn << "\n";
         } else if (op == "keymgr") {
             // KeyManager: register_session_with_material, then rotate_if_needed / rotate_all_due
             std::string sec, mat, ticks; in >> sec >> mat >> ticks;

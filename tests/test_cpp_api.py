@@ -122,12 +122,14 @@ def test_cpp_pow_and_keys_match_reference_golden(api_bin):
         expect.append(f"{c['nonce']} {int(c['valid'])} {int(c['valid_next'])}" if c["found"] else "none")
     for c in pg["handshake_pow"]:
         ops.append(f"handshake_pow {c['initiator']} {c['responder']} {c['public']} {c['difficulty']}")
-        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} 1")
+        dn = c["nonce"] if c["found"] else 2**64 - 1  # Node.cpp drop-in: nonce_out untouched if not found
+        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} 1 {int(c['found'])} {dn}")
     for c in pg["announce_pow"]:
         ops.append("announce_pow " + " ".join(c[k] or "-" for k in ("chunk_id", "peer_id", "endpoint",
                                                                    "manifest_uri", "assigned_shards"))
                    + f" {c['ttl']} {c['difficulty']}")
-        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']}")
+        dn = c["nonce"] if c["found"] else 2**64 - 1
+        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} {int(c['found'])} {dn}")
     for c in pg["session_keys"]:
         ops.append(f"keymgr {c['secret']} {c['material']} {c['rotate_ticks']}")
         expect.append(f"{c['material_key']} {c['rotated_key']} 1")

@@ -1,0 +1,145 @@
+// scalar_latency.cpp -- per-call latency of the reference's scalar crypto API.
+//
+// One source, two builds (oracle/Makefile target `latency`):
+//   oracle/_ref/scalar_latency_gpu : include/ + libenet_crypto.so (every call is a GPU round trip)
+//   oracle/_ref/scalar_latency_ref : /root/reference/include + oracle/_ref/libenet_ref.so (the
+//                                    reference's own CPU code, compiled from its sources)
+// The call shapes are the reference's hot scalar call sites: Message.cpp:305-328 HMAC over a
+// small signed message (98 B is an Acknowledge frame), SessionManager.cpp:374 ChaCha20::apply on
+// a 1500 B frame, KeyExchange.cpp:44 Sha256::digest of 4 B, CryptoManager encrypt of a 4 KiB and
+// 64 KiB chunk, and the Node.cpp:269-292 handshake PoW written as the reference writes it (one
+// Sha256 per attempt).  With ENET_BATCH the drop-in crypto::batch::compute_handshake_pow (one device
+// search) is timed beside it.  Output: one JSON line per case, median and mean microseconds.
+#include "ephemeralnet/crypto/ChaCha20.hpp"
+#include "ephemeralnet/crypto/CryptoManager.hpp"
+#include "ephemeralnet/crypto/HmacSha256.hpp"
+#include "ephemeralnet/crypto/Sha256.hpp"
+#ifdef ENET_BATCH
+#include "ephemeralnet/crypto/Batch.hpp"
+#endif
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+std::uint64_t g_sink = 0;  // printed to stderr at exit so no call is elided
+
+void run(const char* name, std::size_t bytes, int reps, const std::function<void()>& f) {
+    for (int i = 0; i < std::max(3, reps / 10); ++i) f();
+    std::vector<double> us(reps);
+    for (int i = 0; i < reps; ++i) {
+        const auto t0 = Clock::now();
+        f();
+        us[i] = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+    }
+    double sum = 0;
+    for (double u : us) sum += u;
+    std::sort(us.begin(), us.end());
+    std::printf("{\"case\": \"%s\", \"bytes\": %zu, \"reps\": %d, \"median_us\": %.2f, \"mean_us\": %.2f, "
+                "\"p10_us\": %.2f, \"p90_us\": %.2f}\n",
+                name, bytes, reps, us[reps / 2], sum / reps, us[reps / 10], us[(reps * 9) / 10]);
+    std::fflush(stdout);
+}
+
+std::vector<std::uint8_t> pattern(std::size_t n, std::uint8_t s) {
+    std::vector<std::uint8_t> v(n);
+    for (std::size_t i = 0; i < n; ++i) v[i] = static_cast<std::uint8_t>(s + 31 * i + (i >> 7));
+    return v;
+}
+
+// Node.cpp:232-245 / 269-292, as written there: a fresh Sha256 per attempt
+std::array<std::uint8_t, 8> be64(std::uint64_t x) {
+    std::array<std::uint8_t, 8> b{};
+    for (int i = 0; i < 8; ++i) b[i] = static_cast<std::uint8_t>(x >> (56 - 8 * i));
+    return b;
+}
+int lz_bits(const std::array<std::uint8_t, 32>& d) {
+    int t = 0;
+    for (auto b : d) {
+        if (b == 0) { t += 8; continue; }
+        for (int k = 7; k >= 0; --k) { if ((b >> k) & 1) return t; ++t; }
+    }
+    return t;
+}
+std::uint64_t host_loop_pow(const std::array<std::uint8_t, 32>& a, const std::array<std::uint8_t, 32>& b,
+                            std::uint32_t pub, int difficulty, std::uint64_t start, std::uint64_t* attempts) {
+    for (std::uint64_t at = 0; at < 500000; ++at) {
+        ephemeralnet::crypto::Sha256 h;
+        h.update(be64(32));
+        h.update(a);
+        h.update(be64(32));
+        h.update(b);
+        h.update(be64(pub));
+        h.update(be64(start + at));
+        if (lz_bits(h.finalize()) >= difficulty) {
+            *attempts = at + 1;
+            return start + at;
+        }
+    }
+    *attempts = 500000;
+    return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    using namespace ephemeralnet::crypto;
+    const int reps = argc > 1 ? std::atoi(argv[1]) : 200;
+    Key key{};
+    for (int i = 0; i < 32; ++i) key.bytes[i] = static_cast<std::uint8_t>(i * 5 + 1);
+    Nonce nonce{};
+    for (int i = 0; i < 12; ++i) nonce.bytes[i] = static_cast<std::uint8_t>(i + 9);
+    const auto m98 = pattern(98, 1), f1500 = pattern(1500, 2), c4k = pattern(4096, 3), c64k = pattern(65536, 4);
+    const auto mac = HmacSha256::compute(key.bytes, m98);
+    std::vector<std::uint8_t> out;
+    std::array<std::uint8_t, 32> cid{};
+    cid[0] = 7;
+
+    run("hmac_compute", 98, reps, [&] { g_sink += HmacSha256::compute(key.bytes, m98)[0]; });
+    run("hmac_verify", 98, reps, [&] { g_sink += HmacSha256::verify(key.bytes, m98, mac); });
+    run("chacha20_apply", 1500, reps, [&] { ChaCha20::apply(key, nonce, f1500, out, 0); g_sink += out[0]; });
+    run("chacha20_apply", 65536, reps, [&] { ChaCha20::apply(key, nonce, c64k, out, 0); g_sink += out[0]; });
+    const std::array<std::uint8_t, 4> four{1, 2, 3, 4};
+    run("sha256_digest", 4, reps, [&] { g_sink += Sha256::digest(four)[0]; });
+    run("sha256_digest", 65536, reps, [&] { g_sink += Sha256::digest(c64k)[0]; });
+    run("cm_encrypt_with_key", 4096, reps,
+        [&] { g_sink += CryptoManager::encrypt_with_key(key, cid, c4k).data.size(); });
+    run("cm_encrypt_with_key", 65536, reps,
+        [&] { g_sink += CryptoManager::encrypt_with_key(key, cid, c64k).data.size(); });
+
+    // handshake PoW at difficulty 8 (about 256 attempts expected), 5 different peers
+    std::array<std::uint8_t, 32> pa{}, pb{};
+    for (int d : {8, 12}) {
+        for (int i = 0; i < 3; ++i) {
+            pa[0] = static_cast<std::uint8_t>(i + 1);
+            pb[1] = static_cast<std::uint8_t>(d);
+            std::uint64_t att = 0;
+            const auto t0 = Clock::now();
+            const auto n = host_loop_pow(pa, pb, 77u + i, d, 1000003u * i, &att);
+            const double us = std::chrono::duration<double, std::micro>(Clock::now() - t0).count();
+            std::printf("{\"case\": \"handshake_pow_host_loop\", \"difficulty\": %d, \"attempts\": %llu, "
+                        "\"us\": %.1f, \"us_per_attempt\": %.3f, \"nonce\": %llu}\n",
+                        d, (unsigned long long)att, us, us / att, (unsigned long long)n);
+#ifdef ENET_BATCH
+            std::uint64_t dn = 0;
+            const auto t1 = Clock::now();
+            const bool ok = batch::compute_handshake_pow(pa, pb, 77u + i, static_cast<std::uint8_t>(d), dn);
+            const double us1 = std::chrono::duration<double, std::micro>(Clock::now() - t1).count();
+            std::printf("{\"case\": \"handshake_pow_batch_dropin\", \"difficulty\": %d, \"found\": %d, "
+                        "\"us\": %.1f}\n", d, ok ? 1 : 0, us1);
+#endif
+            std::fflush(stdout);
+        }
+    }
+    std::fprintf(stderr, "sink %llu\n", (unsigned long long)g_sink);
+    return 0;
+}
