@@ -64,12 +64,20 @@ def parse():
                          "--chunk-mib chunks (recorded in DESIGN.md, never `value`)")
     ap.add_argument("--chunk-mib", type=int, default=16, help="host pipeline chunk size")
     ap.add_argument("--streams", type=int, default=3, help="host pipeline streams")
-    ap.add_argument("--c5-chunk-mib", type=int, default=64,
+    ap.add_argument("--c5-chunk-mib", type=int, default=256,
                     help="host pipeline chunk size for --c5 (one lane hashes a whole record, so "
                          "mixed batches with HMAC want big chunks)")
+    ap.add_argument("--c5-streams", type=int, default=6,
+                    help="host pipeline streams for --c5 (a chunk's kernel lasts as long as its "
+                         "longest record's serial HMAC, so more chunks in flight)")
     ap.add_argument("--c5", action="store_true",
                     help="SURVEY 8d C5: log-uniform 512 B-64 KiB records, AEAD + fused HMAC-SHA256, "
                          "host-resident (H2D + kernels + D2H), records per GPU = --records")
+    ap.add_argument("--c5-device", action="store_true",
+                    help="C5 shape device-resident (inputs in HBM, one-pass duplex kernel); "
+                         "--c5-order sorted|none picks the record order the kernel walks")
+    ap.add_argument("--c5-order", default="sorted", choices=["sorted", "none"],
+                    help="--c5-device: length-sorted (descending) record order, sort timed inside the step")
     ap.add_argument("--pow-jobs", type=int, default=65536, help="--mode pow: jobs per GPU")
     ap.add_argument("--pow-attempts", type=int, default=4096,
                     help="--mode pow: attempts per job (difficulty 24 = the store clamp, so nearly "
@@ -286,7 +294,7 @@ def c5(args) -> dict:
     mx = int(lens.max()) if n else 0
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
-    pipe = E.Pipeline(local, args.c5_chunk_mib << 20, args.streams)
+    pipe = E.Pipeline(local, args.c5_chunk_mib << 20, args.c5_streams)
 
     def step():
         pipe.aead_hmac_seal(seal_b, ct_h, tags_h, macs_h)
@@ -315,13 +323,66 @@ def c5(args) -> dict:
             "unit": "GiB/s",
             "n_gpus": world,
             "config": {"workload": "C5", "records_total": n_all, "bytes_total": int(lens_all.sum()),
-                       "chunk_mib": args.c5_chunk_mib, "streams": args.streams,
+                       "chunk_mib": args.c5_chunk_mib, "streams": args.c5_streams,
                        "host_buffers": "pinned",
                        "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
     if world > 1:
         dist.destroy_process_group()
     return res
+
+
+def c5_device(args) -> dict:
+    """C5 shape with the batch already in HBM: log-uniform 512 B-64 KiB records, AEAD seal +
+    HMAC-SHA256 then open + verify of both, each direction ONE duplex launch (duplex.hip).  The
+    length sort that balances workgroups (--c5-order sorted) runs on the device inside the timed
+    step.  Single GPU; --records records."""
+    import numpy as np
+    import torch
+
+    import ephemeralnet_amd as E
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    n = args.records
+    lens = np.exp(rng.uniform(np.log(512), np.log(65536), n)).astype(np.int64)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(dev)
+    total = int(lens.sum())
+    g = torch.Generator(device=dev).manual_seed(11)
+    pt = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=g)
+    keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev, generator=g)
+    nonces = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, device=dev, generator=g)
+    ct = torch.empty_like(pt)
+    back = torch.empty_like(pt)
+    tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    macs = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    dl = offs[1:] - offs[:-1]
+
+    def step():
+        order = (torch.argsort(dl, descending=True).to(torch.int32)
+                 if args.c5_order == "sorted" else None)
+        E.aead_hmac_seal(E.Batch(pt, offs, keys, nonces, order=order), ct, tags, macs)
+        E.aead_hmac_open(E.Batch(ct, offs, keys, nonces, order=order), back, tags, macs, ok)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    assert int(ok.sum()) == n and torch.equal(back, pt)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    return {
+        "metric": "GiB/s AEAD + fused HMAC-SHA256 seal+open, mixed 512 B-64 KiB, device-resident",
+        "value": round(total / (ms / 1e3) / 2**30, 2),
+        "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "data": "synthetic",
+        "config": {"workload": "C5 device-resident", "records": n, "bytes_total": total,
+                   "order": args.c5_order, "path": "enet_aead_hmac_seal/open_batch -> duplex_kernel"},
+    }
 
 
 def pow_bench(args) -> dict:
@@ -448,6 +509,9 @@ def main():
         r = pow_bench(args)
         if r:
             print(json.dumps(r), flush=True)
+        return
+    if args.c5_device:
+        print(json.dumps(c5_device(args)))
         return
     if args.c5:
         r = c5(args)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libenet_crypto.so")
 OBJ = os.path.join(PKG, "build")
-SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "frames.hip", "capi.cpp", "crypto_api.cpp", "pipeline.cpp"]
+SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "capi.cpp", "crypto_api.cpp", "pipeline.cpp"]
 HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC",

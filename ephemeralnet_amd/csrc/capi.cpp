@@ -110,27 +110,21 @@ enet::RecParams rec_params(const enet_records* r) {
     return p;
 }
 
-// Uniform batches of session frames go through the fused HMAC + ChaCha20 kernel (frames.hip) in
-// whole workgroups of 256 records; the rest of the batch (and every other shape) through the
-// two-pass path (sha_kernel + records_kernel).  Returns the number of records handled (0 = none).
-// Staging variant 0 (enet_set_staging(0) / ENET_COOP=0) and ENET_FUSED_FRAMES=0 turn it off.
-uint32_t frames_fused(const enet_records* r, bool open, uint32_t hdr, uint8_t* macs, uint8_t* ok,
-                      hipStream_t st, int* err) {
+// Every path with a hash beside the cipher (frames, wire frames, chunk store / fetch with given
+// ids, AEAD + HMAC) runs as ONE pass through the duplex kernel (duplex.hip): any lengths, any
+// alignment, any order.  ENET_DUPLEX=0 or staging variant 0 selects the two-pass path (hash kernel +
+// records kernel) instead.
+bool duplex_on() {
     static const bool on = [] {
-        const char* e = std::getenv("ENET_FUSED_FRAMES");
+        const char* e = std::getenv("ENET_DUPLEX");
         return !(e && e[0] == '0');
     }();
-    *err = ENET_OK;
-    if (!on || enet::staging_variant() == 0 || r->order) return 0;
-    if (!r->max_len_hint || r->total_bytes_hint != (uint64_t)r->count * r->max_len_hint) return 0;
-    const uint64_t over = open ? 32ull + hdr : 0ull;  // frame bytes beyond the message
-    if (r->max_len_hint < over) return 0;
-    const uint64_t Lm = r->max_len_hint - over;
-    if (Lm < enet::kFrameRun || Lm % enet::kFrameRun != 0) return 0;
-    const uint32_t full = r->count / enet::kFrameRecsPerWG * enet::kFrameRecsPerWG;
-    if (!full) return 0;
-    enet::FrameFusedParams p{};
-    p.n = full;
+    return on && enet::staging_variant() != 0;
+}
+
+enet::DuplexParams duplex_params(const enet_records* r) {
+    enet::DuplexParams p{};
+    p.n = r->count;
     p.in = r->in;
     p.in_off = r->in_offsets;
     p.out = r->out;
@@ -138,58 +132,8 @@ uint32_t frames_fused(const enet_records* r, bool open, uint32_t hdr, uint8_t* m
     p.keys = r->keys;
     p.key_stride = r->key_stride;
     p.nonces = r->nonces;
-    p.msg_len = Lm;
-    p.macs = macs;
-    p.ok = ok;
-    *err = hip_status(enet::launch_frames_fused(open, hdr, p, st), "fused frames launch");
-    return full;
-}
-
-// Chunk store / fetch through the fused kernel (frames.hip, CHUNK): uniform batches whose length is
-// a positive multiple of 128 B, whole workgroups of 256 records, caller-given chunk ids (a
-// content-derived counter needs the digest before the first block, so that case stays two-pass).
-// Returns the number of records handled; ENET_FUSED_CHUNKS=0 / staging variant 0 turn it off.
-uint32_t chunks_fused(const enet_records* r, bool fetch, const uint8_t* chunk_ids, uint8_t* digests,
-                      const uint8_t* expect, uint8_t* ok, hipStream_t st, int* err) {
-    static const bool on = [] {
-        const char* e = std::getenv("ENET_FUSED_CHUNKS");
-        return !(e && e[0] == '0');
-    }();
-    *err = ENET_OK;
-    if (!on || !chunk_ids || enet::staging_variant() == 0 || r->order) return 0;
-    if (!r->max_len_hint || r->total_bytes_hint != (uint64_t)r->count * r->max_len_hint) return 0;
-    const uint64_t L = r->max_len_hint;
-    if (L < enet::kFrameRun || L % enet::kFrameRun != 0) return 0;
-    const uint32_t full = r->count / enet::kFrameRecsPerWG * enet::kFrameRecsPerWG;
-    if (!full) return 0;
-    enet::FrameFusedParams p{};
-    p.n = full;
-    p.in = r->in;
-    p.in_off = r->in_offsets;
-    p.out = r->out;
-    p.out_off = r->out_offsets;
-    p.keys = r->keys;
-    p.key_stride = r->key_stride;
-    p.nonces = r->nonces;
-    p.msg_len = L;
-    p.ok = ok;
-    p.chunk_ids = chunk_ids;
-    p.digests = digests;
-    p.expect = expect;
-    *err = hip_status(enet::launch_chunks_fused(fetch, p, st), "fused chunks launch");
-    return full;
-}
-
-// records [k, count) of r as a batch of their own (position-indexed outputs shift with them)
-enet_records tail_records(const enet_records* r, uint32_t k) {
-    enet_records q = *r;
-    q.count = r->count - k;
-    q.in_offsets += k;
-    q.out_offsets += k;
-    q.keys += (size_t)r->key_stride * k;
-    if (q.nonces) q.nonces += 12ull * k;
-    if (q.total_bytes_hint) q.total_bytes_hint = (uint64_t)q.count * r->max_len_hint;
-    return q;
+    p.order = r->order;
+    return p;
 }
 
 uint32_t lanes_for(const enet_records* r) {
@@ -373,7 +317,13 @@ int enet_aead_hmac_seal_batch(const enet_records* r, uint8_t* tags, uint8_t* mac
     if (r->count == 0) return ENET_OK;
     if (!tags || !aligned4(tags) || !macs) return fail(ENET_EINVAL, "tags/macs NULL or misaligned");
     hipStream_t st = (hipStream_t)stream;
-    // HMAC over the plaintext (encode_signed semantics), then the AEAD pass
+    if (duplex_on()) {  // one pass: Poly1305 in the cipher lanes, HMAC in the hash lanes
+        enet::DuplexParams d = duplex_params(r);
+        d.tags = tags;
+        d.macs = macs;
+        return hip_status(enet::launch_duplex(enet::DK_AEADH, false, d, st), "aead_hmac_seal duplex");
+    }
+    // two-pass: HMAC over the plaintext (encode_signed semantics), then the AEAD pass
     enet::ShaParams s{};
     s.n = r->count;
     s.in = r->in;
@@ -396,6 +346,13 @@ int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags, const 
     if (!tags || !aligned4(tags) || !macs || !ok)
         return fail(ENET_EINVAL, "tags/macs/ok NULL or misaligned");
     hipStream_t st = (hipStream_t)stream;
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.tags_in = tags;
+        d.macs_in = macs;
+        d.ok = ok;
+        return hip_status(enet::launch_duplex(enet::DK_AEADH, true, d, st), "aead_hmac_open duplex");
+    }
     enet::RecParams p = rec_params(r);
     p.tag_in = tags;
     p.ok = ok;
@@ -420,11 +377,9 @@ int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tags, const 
 int enet_frame_seal_batch(const enet_records* r, void* stream) {
     if (int e = check_records(r, true)) return e;
     if (r->count == 0) return ENET_OK;
-    int fe;
-    if (uint32_t k = frames_fused(r, false, 0, nullptr, nullptr, (hipStream_t)stream, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records q = tail_records(r, k);
-        return enet_frame_seal_batch(&q, stream);
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        return hip_status(enet::launch_duplex(enet::DK_FRAME, false, d, (hipStream_t)stream), "frame_seal duplex");
     }
     // 1) MAC = HMAC-SHA256(K, m) written in clear at the tail of each output record
     enet::ShaParams s{};
@@ -448,11 +403,11 @@ int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, voi
     if (r->count == 0) return ENET_OK;
     if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "frame_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
-    int fe;
-    if (uint32_t k = frames_fused(r, true, 0, macs, ok, st, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records q = tail_records(r, k);
-        return enet_frame_open_batch(&q, macs + 32ull * k, ok + k, stream);
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.macs = macs;
+        d.ok = ok;
+        return hip_status(enet::launch_duplex(enet::DK_FRAME, true, d, st), "frame_open duplex");
     }
     // 1) decrypt: message bytes to out, MAC bytes to macs
     enet::RecParams p = rec_params(r);
@@ -482,11 +437,11 @@ int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids, uint
         return fail(ENET_EINVAL, "chunk_store: chunk_hashes NULL or misaligned");
     if (chunk_ids && !aligned4(chunk_ids)) return fail(ENET_EINVAL, "chunk_store: chunk_ids misaligned");
     hipStream_t st = (hipStream_t)stream;
-    int fe;
-    if (uint32_t k = chunks_fused(r, false, chunk_ids, chunk_hashes, nullptr, nullptr, st, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records q = tail_records(r, k);
-        return enet_chunk_store_batch(&q, chunk_ids + 32ull * k, chunk_hashes + 32ull * k, stream);
+    if (chunk_ids && duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.chunk_ids = chunk_ids;
+        d.digests = chunk_hashes;
+        return hip_status(enet::launch_duplex(enet::DK_CHUNK, false, d, st), "chunk_store duplex");
     }
     // 1) chunk_hash = SHA-256(pt) (Node.cpp:1414; = derive_chunk_id, StoreProof.cpp:75-78)
     enet::ShaParams s{};
@@ -512,12 +467,12 @@ int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
     if (!chunk_ids || !aligned4(chunk_ids) || !chunk_hashes || !ok)
         return fail(ENET_EINVAL, "chunk_fetch: NULL/misaligned chunk_ids, NULL hashes or ok");
     hipStream_t st = (hipStream_t)stream;
-    int fe;
-    if (uint32_t k = chunks_fused(r, true, chunk_ids, nullptr, chunk_hashes, ok, st, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records q = tail_records(r, k);
-        return enet_chunk_fetch_batch(&q, chunk_ids + 32ull * k, chunk_hashes + 32ull * k, ok + k,
-                                      stream);
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.chunk_ids = chunk_ids;
+        d.expect = chunk_hashes;
+        d.ok = ok;
+        return hip_status(enet::launch_duplex(enet::DK_CHUNK, true, d, st), "chunk_fetch duplex");
     }
     // 1) decrypt_with_key (CryptoManager.cpp:49-58)
     enet::RecParams p = rec_params(r);
@@ -542,11 +497,10 @@ int enet_wire_seal_batch(const enet_records* r, void* stream) {
     if (int e = check_records(r, true)) return e;
     if (r->count == 0) return ENET_OK;
     hipStream_t st = (hipStream_t)stream;
-    int fe;
-    if (uint32_t k = frames_fused(r, false, kWireHeader, nullptr, nullptr, st, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records q = tail_records(r, k);
-        return enet_wire_seal_batch(&q, stream);
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.hdr = kWireHeader;
+        return hip_status(enet::launch_duplex(enet::DK_FRAME, false, d, st), "wire_seal duplex");
     }
     // 1) MAC = HMAC-SHA256(K, m) in clear at the tail of each frame body
     enet::ShaParams s{};
@@ -574,11 +528,12 @@ int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void
     if (int e = check_records(&q, true)) return e;
     if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "wire_open: NULL/misaligned macs or NULL ok");
     hipStream_t st = (hipStream_t)stream;
-    int fe;
-    if (uint32_t k = frames_fused(&q, true, kWireHeader, macs, ok, st, &fe)) {
-        if (fe || k == r->count) return fe;
-        const enet_records t = tail_records(r, k);
-        return enet_wire_open_batch(&t, macs + 32ull * k, ok + k, stream);
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(&q);
+        d.hdr = kWireHeader;
+        d.macs = macs;
+        d.ok = ok;
+        return hip_status(enet::launch_duplex(enet::DK_FRAME, true, d, st), "wire_open duplex");
     }
     enet::RecParams p = rec_params(&q);
     p.nonces = nullptr;

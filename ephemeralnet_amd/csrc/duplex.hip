@@ -1,0 +1,448 @@
+// duplex.hip -- one HBM pass of cipher + hash over ANY batch of records (gfx950).
+//
+// Three reference paths encrypt a record and hash the same bytes:
+//   frames   protocol::encode_signed + SessionManager::send (Message.cpp:305-311,
+//            SessionManager.cpp:362-387): body = ChaCha20_{K,N,0}(m || HMAC-SHA256_K(m)), optionally
+//            behind the nonce(12) || BE32(|body|) wire header; receive reverses it
+//            (SessionManager.cpp:760-822, Message.cpp:313-328);
+//   chunks   Node::store_chunk / fetch_chunk (Node.cpp:1414-1417, 1644-1655): ChaCha20 from counter
+//            LE32(chunk_id) (CryptoManager.cpp:8-13, 38-58) and SHA-256(m) (= derive_chunk_id);
+//   AEAD+MAC RFC 8439 ChaCha20-Poly1305 with HMAC-SHA256_K(m) beside the tag (BASELINE config 5).
+// SHA-256 is serial inside a record, so a record gets one lane for its hash; a 512-thread workgroup
+// owns 256 records and splits into 4 "cipher" waves and 4 "hash" waves (waves w and w + 4 share a
+// SIMD and a record set: lane l of both serves record 64 w + l).  The cipher lane streams its
+// record in 128-byte stages (one stage prefetched in registers), runs ChaCha20 (and Poly1305 over
+// the ciphertext), stores, and hands every stage's plaintext to the hash lane through a
+// double-buffered LDS slab -- one workgroup barrier per stage.  The plaintext is never re-read
+// from HBM.
+//
+// Unlike frames.hip (uniform lengths, multiple of 128 B, whole workgroups), nothing is assumed:
+// every lane reads its own record's offsets, lengths may differ lane to lane (a workgroup runs
+// the stages of its longest record; `order` -- e.g. length-sorted -- keeps workgroups balanced),
+// record starts may have any alignment, and the ragged end of a record (< 128 bytes, plus the
+// 32-byte MAC of a frame body) goes through a 160-byte LDS tail slot per record:
+//   seal  T1 cipher loads the message tail and parks it in the slot (chunks / AEAD also encrypt
+//            and store it); T2 hash lane hashes it (masked, SHA padding) and finishes the digest --
+//            frames put the MAC bytes right behind the message tail in the slot; T3 (frames) the
+//            cipher lane encrypts message tail || MAC as one run of body bytes and stores it.
+//   open  T1 cipher loads the body tail, checks Poly1305 (AEAD), decrypts, stores the message
+//            tail, parks it (frames: with the decrypted MAC) in the slot; T2 hash lane finishes,
+//            compares, writes ok, and zeroes a failed record's output.
+// A record whose output length does not match its input (frames: out = in + 32 + hdr) is not
+// processed: its output range is zeroed and, when opening, ok = 0.
+#include "enet_device.hpp"
+#include "enet_internal.hpp"
+
+namespace enet {
+
+namespace {
+
+constexpr uint32_t kDThreads = 512;         // 4 cipher waves + 4 hash waves
+constexpr uint32_t kDR = kDuplexRecsPerWG;  // records per workgroup
+constexpr uint32_t kRun = 128;              // bytes per stage and record
+constexpr uint32_t kBuf = kDR * kRun;       // one stage of the workgroup: 32 KB
+
+// all waves: this wave's LDS traffic is done, then meet
+#define ENET_DX_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// keep bytes [0, r) of the LE byte string in w[0..N)
+template <int N>
+__device__ __forceinline__ void keep_le(uint32_t* w, uint32_t r) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        const uint32_t b = 4u * j;
+        const uint32_t m = b + 4u <= r ? 0xffffffffu : (b >= r ? 0u : (1u << (8u * (r - b))) - 1u);
+        w[j] &= m;
+    }
+}
+
+__device__ __forceinline__ void zero_bytes(uint8_t* p, uint64_t n) {
+    const uint32_t z[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint64_t o = 0; o < n; o += 64) store_block(p + o, (uint32_t)min<uint64_t>(64, n - o), z);
+}
+
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { return ld32(p); }
+
+}  // namespace
+
+template <int KIND, bool OPEN>
+__device__ __forceinline__ void duplex_body(const DuplexParams& p) {
+    __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kBuf];  // stage slabs (64 KB)
+    __shared__ __attribute__((aligned(16))) uint8_t text[kDR * 32];  // tail slot bytes 128..159
+    __shared__ uint32_t tmax_s;
+
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool cipher = wave < 4;
+    const uint32_t rl = 64u * (wave & 3u) + lane;
+    const uint32_t pos = blockIdx.x * kDR + rl;
+    const bool live = pos < p.n;
+    const uint32_t rec = live ? (p.order ? p.order[pos] : pos) : 0u;
+    const uint32_t H = KIND == DK_FRAME ? p.hdr : 0u;
+
+    // ---- geometry (both lanes of a record compute it)
+    uint64_t ib = 0, Li = 0, ob = 0, Lo = 0;
+    if (live) {
+        ib = p.in_off[rec];
+        Li = p.in_off[rec + 1] - ib;
+        ob = p.out_off[rec];
+        Lo = p.out_off[rec + 1] - ob;
+    }
+    uint64_t Lm = 0;  // message bytes
+    bool valid = live;
+    if (KIND == DK_FRAME && !OPEN) {
+        Lm = Li;
+        valid = valid && Lo == Li + 32u + H;
+    } else if (KIND == DK_FRAME) {  // frames shorter than [hdr] + MAC fail (Message.cpp:315)
+        valid = valid && Li >= 32ull + H;
+        Lm = valid ? Li - 32u - H : 0;
+        valid = valid && Lo == Lm;
+    } else {
+        Lm = Li;
+        valid = valid && Lo == Li;
+    }
+    if (!valid) Lm = 0;
+    const uint32_t Ts = (uint32_t)(Lm / kRun);         // whole stages
+    const uint32_t r = (uint32_t)(Lm - (uint64_t)kRun * Ts);  // ragged end, < 128
+    const uint64_t tb = (uint64_t)kRun * Ts;            // message offset of the ragged end
+
+    if (threadIdx.x == 0) tmax_s = 0;
+    __syncthreads();
+    if (cipher && Ts) atomicMax(&tmax_s, Ts);
+    __syncthreads();
+    const uint32_t Tmax = __builtin_amdgcn_readfirstlane(tmax_s);
+
+    const uint32_t msw = (lane >> 1) & 7u;  // 16-byte chunk swizzle of a 128-byte run in LDS
+    uint8_t* const trow = ptb + (Tmax & 1u) * kBuf + rl * kRun;  // tail slot bytes 0..127
+    uint8_t* const xrow = text + rl * 32u;                       // tail slot bytes 128..159
+    auto slot_byte = [&](uint32_t i) -> uint8_t* { return i < kRun ? trow + i : xrow + (i - kRun); };
+
+    uint32_t kw[8];
+    {
+        const uint8_t* kp = p.keys + (size_t)p.key_stride * rec;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kw[i] = live ? reinterpret_cast<const uint32_t*>(kp)[i] : 0u;
+    }
+
+    if (cipher) {
+        // ============================================================== cipher lane
+        const uint8_t* src = p.in + ib + (OPEN ? H : 0u);
+        uint8_t* dst = p.out + ob + (OPEN ? 0u : H);
+        const uint32_t off0 = OPEN ? H : 0u;  // offset of src inside the input record
+        uint32_t nw[3];
+        if (OPEN && KIND == DK_FRAME && H) {  // nonce = the frame's first 12 bytes (SessionManager.cpp:815-822)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nw[i] = valid ? ld32u(p.in + ib + 4 * i) : 0u;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nw[i] = live ? ld32u(p.nonces + 12ull * rec + 4 * i) : 0u;
+        }
+        ChachaRecord R;
+        chacha_record_init(R, kw, nw);
+        // ChaCha20::apply start counter: frames 0, chunks LE32(chunk_id) (u32 wrap), AEAD 1
+        const uint32_t c0 = KIND == DK_FRAME ? 0u
+                          : KIND == DK_CHUNK ? (live ? ld32u(p.chunk_ids + 32ull * rec) : 0u)
+                                             : 1u;
+        PolyR32 PR{};
+        uint32_t h[5] = {0, 0, 0, 0, 0}, pad[4] = {0, 0, 0, 0};
+        if (KIND == DK_AEADH) {  // one-time key = keystream block 0 (RFC 8439 2.6)
+            uint32_t otk[16];
+            chacha_block(R, 0u, otk);
+            PR = polyr32_make(otk[0], otk[1], otk[2], otk[3]);
+            pad[0] = otk[4]; pad[1] = otk[5]; pad[2] = otk[6]; pad[3] = otk[7];
+        }
+        auto poly_words = [&](const uint32_t* w, uint32_t blocks) {  // blocks <= 8
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q)
+                if (q < blocks) poly32_block(h, PR, w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3], 1u);
+        };
+
+        uint32_t pf[32];
+        auto load_run = [&](uint32_t s) {
+            const uint4* q = reinterpret_cast<const uint4*>(src + (uint64_t)kRun * s);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = q[i];
+                pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+            }
+        };
+        auto put_run = [&](uint8_t* d, const uint32_t* v) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<uint4*>(d + 16u * (k ^ msw)) =
+                    make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+        };
+        if (Ts > 0) load_run(0);
+        for (uint32_t s = 0; s < Tmax; ++s) {
+            if (s < Ts) {
+                uint32_t x[32];
+#pragma unroll
+                for (int i = 0; i < 32; ++i) x[i] = pf[i];
+                if (s + 1 < Ts) load_run(s + 1);
+                uint8_t* const pt = ptb + (s & 1u) * kBuf + rl * kRun;
+                if (!OPEN) put_run(pt, x);  // plaintext for the hash lane
+                if (KIND == DK_AEADH && OPEN) poly_words(x, 8);
+                {
+                    uint32_t ka[16], kb[16];
+                    chacha_block2(R, c0 + 2u * s, c0 + 2u * s + 1u, ka, kb);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
+                }
+                if (KIND == DK_AEADH && !OPEN) poly_words(x, 8);
+                if (OPEN) put_run(pt, x);
+                uint4* o = reinterpret_cast<uint4*>(dst + (uint64_t)kRun * s);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+            }
+            ENET_DX_BARRIER();  // stage s plaintext is in ptb[s & 1]
+        }
+
+        // ---- ragged end
+        const uint32_t tin = (OPEN && KIND == DK_FRAME) ? r + 32u : r;  // body-tail bytes read now
+        uint32_t w[48];
+#pragma unroll
+        for (int i = 0; i < 48; ++i) w[i] = 0u;
+        if (valid && tin) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if (tin > 64u * k) {
+                    const uint32_t nk = min(64u, tin - 64u * k);
+                    load_block(src + tb + 64u * k, nk, w + 16 * k, off0 + tb + 64u * k + nk >= 16u);
+                }
+            }
+        }
+        uint32_t ks[48];
+#pragma unroll
+        for (int i = 32; i < 48; ++i) ks[i] = 0u;  // the third block is only made when a body needs it
+        if (valid && (tin || (!OPEN && KIND == DK_FRAME))) {
+            chacha_block2(R, c0 + 2u * Ts, c0 + 2u * Ts + 1u, ks, ks + 16);
+            if (KIND == DK_FRAME && r + 32u > 128u) chacha_block(R, c0 + 2u * Ts + 2u, ks + 32);
+        }
+        if (!OPEN) {
+            if (valid) {
+                // T1: the message tail to the hash lane
+#pragma unroll
+                for (int j = 0; j < 32; ++j) reinterpret_cast<uint32_t*>(trow)[j] = w[j];
+                if (KIND != DK_FRAME && r) {
+#pragma unroll
+                    for (int j = 0; j < 32; ++j) w[j] ^= ks[j];
+                    store_block(dst + tb, min(r, 64u), w);
+                    if (r > 64u) store_block(dst + tb + 64, r - 64u, w + 16);
+                    if (KIND == DK_AEADH) {
+                        keep_le<32>(w, r);
+                        poly_words(w, (r + 15u) >> 4);
+                    }
+                }
+                if (KIND == DK_AEADH) {
+                    poly32_block(h, PR, 0u, 0u, (uint32_t)Lm, (uint32_t)(Lm >> 32), 1u);
+                    uint32_t l[5], tag[4];
+                    h32_to_limbs(h, l);
+                    pfinish(l, pad, tag);
+                    *reinterpret_cast<uint4*>(p.tags + 16ull * rec) = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+                }
+            }
+            ENET_DX_BARRIER();  // T1
+            ENET_DX_BARRIER();  // T2: frames -- the MAC sits behind the message tail in the slot
+            if (KIND == DK_FRAME && valid) {
+                // T3: body tail = message tail || MAC, one run of body bytes
+                const uint32_t t = r + 32u;
+#pragma unroll
+                for (int j = 0; j < 32; ++j) w[j] = reinterpret_cast<const uint32_t*>(trow)[j] ^ ks[j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) w[32 + j] = reinterpret_cast<const uint32_t*>(xrow)[j] ^ ks[32 + j];
+                store_block(dst + tb, min(t, 64u), w);
+                if (t > 64u) store_block(dst + tb + 64, min(t - 64u, 64u), w + 16);
+                if (t > 128u) store_block(dst + tb + 128, t - 128u, w + 32);
+                if (H) {  // nonce(12) || BE32(|body|) (SessionManager.cpp:376-385)
+                    *reinterpret_cast<uint4*>(p.out + ob) =
+                        make_uint4(nw[0], nw[1], nw[2], bswap32((uint32_t)(Lm + 32u)));
+                }
+            }
+        } else {
+            if (valid) {
+                uint32_t aok = 1;
+                if (KIND == DK_AEADH) {  // Poly1305 over the ciphertext (zero beyond r), then lengths
+                    poly_words(w, (r + 15u) >> 4);
+                    poly32_block(h, PR, 0u, 0u, (uint32_t)Lm, (uint32_t)(Lm >> 32), 1u);
+                    uint32_t l[5], tag[4];
+                    h32_to_limbs(h, l);
+                    pfinish(l, pad, tag);
+                    const uint8_t* tp = p.tags_in + 16ull * rec;
+                    aok = ((tag[0] ^ ld32u(tp)) | (tag[1] ^ ld32u(tp + 4)) | (tag[2] ^ ld32u(tp + 8)) |
+                           (tag[3] ^ ld32u(tp + 12))) == 0u;
+                }
+                if (tin) {
+#pragma unroll
+                    for (int j = 0; j < 40; ++j) w[j] ^= ks[j];
+                }
+                if (r) {
+                    store_block(dst + tb, min(r, 64u), w);
+                    if (r > 64u) store_block(dst + tb + 64, r - 64u, w + 16);
+                }
+#pragma unroll
+                for (int j = 0; j < 32; ++j) reinterpret_cast<uint32_t*>(trow)[j] = w[j];
+                if (KIND == DK_FRAME) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) reinterpret_cast<uint32_t*>(xrow)[j] = w[32 + j];
+                }
+                if (KIND == DK_AEADH) xrow[31] = (uint8_t)aok;
+            }
+            // the plaintext stores are complete before a hash lane may zero them on failure
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ENET_DX_BARRIER();  // T1
+        }
+    } else {
+        // ============================================================== hash lane
+        // frames / AEAD: HMAC-SHA256 (HmacSha256.cpp:11-39) with the 32-byte record key;
+        // chunks: SHA-256 (Sha256::digest, Sha256.cpp:66-132)
+        uint32_t kb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kb[i] = bswap32(kw[i]);
+        uint32_t st[8], x[16];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st[i] = kShaIV[i];
+        if (KIND != DK_CHUNK) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x36363636u;
+            sha256_compress(st, x);
+        }
+        for (uint32_t s = 0; s < Tmax; ++s) {
+            ENET_DX_BARRIER();
+            if (s < Ts) {
+                const uint8_t* pt = ptb + (s & 1u) * kBuf + rl * kRun;
+#pragma unroll
+                for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint4 v = *reinterpret_cast<const uint4*>(pt + 16u * ((4 * hb + k) ^ msw));
+                        x[4 * k] = bswap32(v.x); x[4 * k + 1] = bswap32(v.y);
+                        x[4 * k + 2] = bswap32(v.z); x[4 * k + 3] = bswap32(v.w);
+                    }
+                    sha256_compress(st, x);
+                }
+            }
+        }
+        ENET_DX_BARRIER();  // T1: the ragged end is in the slot
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // digest as LE words of its bytes
+        if (valid) {
+            // message tail, 0x80, zeros, BE64 bit length of [ipad ||] m
+            const uint64_t bits = ((KIND == DK_CHUNK ? 0ull : 64ull) + Lm) * 8ull;
+            const uint32_t nb = (r + 9u + 63u) >> 6;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                if ((uint32_t)k < nb) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const uint32_t b = 64u * k + 4u * i;
+                        const uint32_t v = k < 2 ? bswap32(reinterpret_cast<const uint32_t*>(trow)[16 * k + i]) : 0u;
+                        const uint32_t m = b + 4u <= r ? 0xffffffffu : (b >= r ? 0u : 0xffffffffu << (8u * (4u - (r - b))));
+                        x[i] = (v & m) | ((r >> 2) == (b >> 2) ? 0x80000000u >> (8u * (r & 3u)) : 0u);
+                    }
+                    if ((uint32_t)k == nb - 1u) {
+                        x[14] = (uint32_t)(bits >> 32);
+                        x[15] = (uint32_t)bits;
+                    }
+                    sha256_compress(st, x);
+                }
+            }
+            if (KIND != DK_CHUNK) {
+                uint32_t inner[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) inner[i] = st[i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) st[i] = kShaIV[i];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x5c5c5c5cu;
+                sha256_compress(st, x);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) x[i] = inner[i];
+                x[8] = 0x80000000u;
+#pragma unroll
+                for (int i = 9; i < 15; ++i) x[i] = 0u;
+                x[15] = (64 + 32) * 8;
+                sha256_compress(st, x);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) d[i] = bswap32(st[i]);
+        }
+        if (!OPEN) {
+            if (valid) {
+                if (KIND == DK_FRAME) {  // the MAC follows the message tail in the slot
+                    for (uint32_t i = 0; i < 32u; ++i) *slot_byte(r + i) = (uint8_t)(d[i >> 2] >> (8u * (i & 3u)));
+                } else {
+                    uint8_t* dp = (KIND == DK_CHUNK ? p.digests : p.macs) + 32ull * rec;
+                    reinterpret_cast<uint4*>(dp)[0] = make_uint4(d[0], d[1], d[2], d[3]);
+                    reinterpret_cast<uint4*>(dp)[1] = make_uint4(d[4], d[5], d[6], d[7]);
+                }
+            } else if (live) {
+                zero_bytes(p.out + ob, Lo);
+            }
+            ENET_DX_BARRIER();  // T2
+        } else if (live) {
+            uint32_t diff = valid ? 0u : 1u;
+            if (valid) {
+                if (KIND == DK_FRAME) {  // HmacSha256::verify (HmacSha256.cpp:41-54)
+                    uint32_t e[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) v |= (uint32_t)*slot_byte(r + 4u * j + b) << (8 * b);
+                        e[j] = v;
+                        diff |= v ^ d[j];
+                    }
+                    uint8_t* mp = p.macs + 32ull * rec;
+                    reinterpret_cast<uint4*>(mp)[0] = make_uint4(e[0], e[1], e[2], e[3]);
+                    reinterpret_cast<uint4*>(mp)[1] = make_uint4(e[4], e[5], e[6], e[7]);
+                    if (H) {  // the length field must give the body (SessionManager.cpp:770-796)
+                        const uint32_t be = bswap32(ld32u(p.in + ib + 12));
+                        if ((uint64_t)be != Li - H) diff = 1;
+                    }
+                } else {
+                    const uint8_t* ep = (KIND == DK_CHUNK ? p.expect : p.macs_in) + 32ull * rec;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) diff |= ld32u(ep + 4 * j) ^ d[j];
+                    if (KIND == DK_AEADH && xrow[31] == 0) diff = 1;
+                }
+            }
+            p.ok[rec] = diff == 0u ? 1 : 0;
+            if (diff != 0u) zero_bytes(p.out + ob, Lo);  // no plaintext for a failed record
+        }
+    }
+}
+
+// Frames and chunks fit 128 VGPRs, so two workgroups share a CU (LDS 72 KB each) when the batch
+// has more than 256 workgroups (C3: 1 M frames, 358 -> 388 GiB/s).  The AEAD + HMAC body would
+// spill at 128, so it keeps one workgroup per CU.
+template <int KIND, bool OPEN>
+__global__ __launch_bounds__(kDThreads) __attribute__((amdgpu_waves_per_eu(4))) void duplex_kernel(DuplexParams p) {
+    duplex_body<KIND, OPEN>(p);
+}
+template <int KIND, bool OPEN>
+__global__ __launch_bounds__(kDThreads) void duplex_kernel_wide(DuplexParams p) {
+    duplex_body<KIND, OPEN>(p);
+}
+
+hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s) {
+    const uint32_t blocks = (p.n + kDR - 1) / kDR;
+    if (blocks == 0) return hipSuccess;
+#define ENET_DX_LAUNCH(K, O) \
+    hipLaunchKernelGGL((duplex_kernel<K, O>), dim3(blocks), dim3(kDThreads), 0, s, p)
+    switch (kind * 2 + (open ? 1 : 0)) {
+        case DK_FRAME * 2: ENET_DX_LAUNCH(DK_FRAME, false); break;
+        case DK_FRAME * 2 + 1: ENET_DX_LAUNCH(DK_FRAME, true); break;
+        case DK_CHUNK * 2: ENET_DX_LAUNCH(DK_CHUNK, false); break;
+        case DK_CHUNK * 2 + 1: ENET_DX_LAUNCH(DK_CHUNK, true); break;
+        case DK_AEADH * 2:
+            hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, false>), dim3(blocks), dim3(kDThreads), 0, s, p);
+            break;
+        case DK_AEADH * 2 + 1:
+            hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, true>), dim3(blocks), dim3(kDThreads), 0, s, p);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+#undef ENET_DX_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace enet

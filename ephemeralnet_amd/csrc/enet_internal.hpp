@@ -84,30 +84,35 @@ struct ShaParams {
 };
 hipError_t launch_sha(const ShaParams& p, hipStream_t s);
 
-// Fused HMAC-SHA256 + ChaCha20 over uniform batches of session frames (frames.hip): every
-// record holds msg_len message bytes (a multiple of kFrameRun), records are contiguous in both
-// arenas, seal writes [hdr] || ChaCha20(m || HMAC(m)) and open the reverse.
-constexpr uint32_t kFrameRecsPerWG = 256;
-constexpr uint32_t kFrameRun = 128;
-struct FrameFusedParams {
-    uint32_t n;  // records, a multiple of kFrameRecsPerWG
+// One-pass cipher + hash over ANY batch (duplex.hip): every record length, every alignment, any
+// order.  A cipher lane and a hash lane per record; the message crosses HBM once.
+enum DuplexKind : int {
+    DK_FRAME = 0,  // frames: body = ChaCha20_{K,N,0}(m || HMAC_K(m)), [hdr] in front
+    DK_CHUNK = 1,  // chunk store / fetch: ChaCha20 from LE32(chunk_id) + SHA-256(m)
+    DK_AEADH = 2,  // RFC 8439 AEAD (counter 1, Poly1305 over the ciphertext) + HMAC_K(m)
+};
+constexpr uint32_t kDuplexRecsPerWG = 256;
+struct DuplexParams {
+    uint32_t n;
     const uint8_t* in;
     const uint64_t* in_off;
     uint8_t* out;
     const uint64_t* out_off;
     const uint8_t* keys;
     uint32_t key_stride;
-    const uint8_t* nonces;  // seal and frame open: [n][12]; wire open reads the frame header
-    uint64_t msg_len;
-    uint8_t* macs;  // open: decrypted MACs [n][32]
-    uint8_t* ok;    // open: verdicts
-    const uint8_t* chunk_ids;  // chunks: [n][32], start counter LE32(id[0..3])
-    uint8_t* digests;          // chunk store: SHA-256(m) [n][32]
-    const uint8_t* expect;     // chunk fetch: expected SHA-256 [n][32]
+    const uint8_t* nonces;     // [rec][12]; wire open (hdr 16) reads the frame header instead
+    const uint32_t* order;     // nullable: position -> record (e.g. length-sorted)
+    uint32_t hdr;              // frames: 0 or 16 (nonce || BE32 body length)
+    const uint8_t* chunk_ids;  // chunks: start counter LE32(id[0..3])
+    uint8_t* digests;          // chunk store: SHA-256(m)
+    const uint8_t* expect;     // chunk fetch: expected SHA-256(m)
+    uint8_t* macs;             // frame open: decrypted MACs; AEADH seal: HMAC_K(m)
+    const uint8_t* macs_in;    // AEADH open: expected HMAC_K(m)
+    uint8_t* tags;             // AEADH seal: Poly1305 tags
+    const uint8_t* tags_in;    // AEADH open: expected tags
+    uint8_t* ok;               // open / fetch verdicts
 };
-hipError_t launch_frames_fused(bool open, uint32_t hdr, const FrameFusedParams& p, hipStream_t s);
-// the same kernel for the chunk store (SHA-256 + ChaCha20) / fetch (ChaCha20 + SHA-256 check)
-hipError_t launch_chunks_fused(bool fetch, const FrameFusedParams& p, hipStream_t s);
+hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s);
 
 // Proof-of-work search / check (pow.hip): SHA-256(prefix_i || BE64(candidate)).
 struct PowParams {

@@ -1,8 +1,7 @@
-"""GPU parity of the fused chunk store / fetch kernel (frames.hip, CHUNK) against the CPU oracle
-and hashlib: uniform batches with caller-given chunk ids whose length is a multiple of 128 bytes
-go through it in whole workgroups of 256 records, the rest of the batch through the two-pass path
-(sha_kernel + records_kernel); staging variant 0 forces the two-pass path for every record, so
-both must give the same bytes.  Reference: Node::store_chunk (src/core/Node.cpp:1414-1417:
+"""GPU parity of the one-pass chunk store / fetch path (duplex.hip, DK_CHUNK) against the CPU
+oracle and hashlib on uniform batches with caller-given chunk ids (content-derived ids stay
+two-pass: the counter needs the digest first); staging variant 0 forces the two-pass path
+(sha_kernel + records_kernel), so both must give the same bytes.  Reference: Node::store_chunk (src/core/Node.cpp:1414-1417:
 chunk_hash = Sha256::digest(data), encrypt_with_key(chunk_key, chunk_id, data)) and
 Node::fetch_chunk (:1644-1655: decrypt_with_key, then the hash check); ChaCha20 start counter
 LE32(chunk_id[0..3]) (src/crypto/CryptoManager.cpp:8-13).  Bit-exact comparisons throughout."""

@@ -1,10 +1,9 @@
-"""GPU parity of the fused HMAC-SHA256 + ChaCha20 frame kernel (frames.hip) against the CPU
-oracle: uniform batches whose message length is a multiple of 128 bytes go through it in whole
-workgroups of 256 records, the rest of the batch through the two-pass path (sha_kernel +
-records_kernel); staging variant 0 forces the two-pass path for every record, so both must give
-the same bytes.  Reference: SessionManager::send / receive_loop framing
-(src/network/SessionManager.cpp:362-387, :760-822), encode_signed / decode_signed
-(src/protocol/Message.cpp:305-328).  Bit-exact comparisons throughout."""
+"""GPU parity of the one-pass HMAC-SHA256 + ChaCha20 frame path (duplex.hip, DK_FRAME) against
+the CPU oracle on uniform batches (round 1's fused-kernel shapes: multiples of 128 B, whole and
+partial workgroups, unaligned arenas); staging variant 0 forces the two-pass path (sha_kernel +
+records_kernel), so both must give the same bytes.  Ragged and mixed shapes: test_gpu_duplex.py.
+Reference: SessionManager::send / receive_loop framing (src/network/SessionManager.cpp:362-387,
+:760-822), encode_signed / decode_signed (src/protocol/Message.cpp:305-328).  Bit-exact."""
 import dataclasses
 
 import numpy as np
