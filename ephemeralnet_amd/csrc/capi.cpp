@@ -133,6 +133,7 @@ enet::DuplexParams duplex_params(const enet_records* r) {
     p.key_stride = r->key_stride;
     p.nonces = r->nonces;
     p.order = r->order;
+    p.uniform = r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint;
     return p;
 }
 

@@ -33,14 +33,13 @@
 #include "enet_device.hpp"
 #include "enet_internal.hpp"
 
+#include <cstdlib>
+
 namespace enet {
 
 namespace {
 
-constexpr uint32_t kDThreads = 512;         // 4 cipher waves + 4 hash waves
-constexpr uint32_t kDR = kDuplexRecsPerWG;  // records per workgroup
-constexpr uint32_t kRun = 128;              // bytes per stage and record
-constexpr uint32_t kBuf = kDR * kRun;       // one stage of the workgroup: 32 KB
+constexpr uint32_t kRun = 128;  // bytes per stage and record
 
 // all waves: this wave's LDS traffic is done, then meet
 #define ENET_DX_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
@@ -65,17 +64,20 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* p) { return ld32(p); }
 
 }  // namespace
 
-template <int KIND, bool OPEN>
+// RPW records per workgroup: RPW / 64 cipher waves + RPW / 64 hash waves.
+template <int KIND, bool OPEN, int RPW>
 __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
-    __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kBuf];  // stage slabs (64 KB)
-    __shared__ __attribute__((aligned(16))) uint8_t text[kDR * 32];  // tail slot bytes 128..159
+    constexpr uint32_t kW = RPW / 64;          // waves per role
+    constexpr uint32_t kBuf = RPW * kRun;      // one stage of the workgroup (32 KB at 256 records)
+    __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kBuf];  // stage slabs
+    __shared__ __attribute__((aligned(16))) uint8_t text[RPW * 32];  // tail slot bytes 128..159
     __shared__ uint32_t tmax_s;
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    const bool cipher = wave < 4;
-    const uint32_t rl = 64u * (wave & 3u) + lane;
-    const uint32_t pos = blockIdx.x * kDR + rl;
+    const bool cipher = wave < kW;
+    const uint32_t rl = 64u * (wave % kW) + lane;
+    const uint32_t pos = blockIdx.x * RPW + rl;
     const bool live = pos < p.n;
     const uint32_t rec = live ? (p.order ? p.order[pos] : pos) : 0u;
     const uint32_t H = KIND == DK_FRAME ? p.hdr : 0u;
@@ -414,35 +416,43 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
 // Frames and chunks fit 128 VGPRs, so two workgroups share a CU (LDS 72 KB each) when the batch
 // has more than 256 workgroups (C3: 1 M frames, 358 -> 388 GiB/s).  The AEAD + HMAC body would
 // spill at 128, so it keeps one workgroup per CU.
-template <int KIND, bool OPEN>
-__global__ __launch_bounds__(kDThreads) __attribute__((amdgpu_waves_per_eu(4))) void duplex_kernel(DuplexParams p) {
-    duplex_body<KIND, OPEN>(p);
+template <int KIND, bool OPEN, int RPW>
+__global__ __launch_bounds__(2 * RPW) __attribute__((amdgpu_waves_per_eu(4))) void duplex_kernel(DuplexParams p) {
+    duplex_body<KIND, OPEN, RPW>(p);
 }
-template <int KIND, bool OPEN>
-__global__ __launch_bounds__(kDThreads) void duplex_kernel_wide(DuplexParams p) {
-    duplex_body<KIND, OPEN>(p);
+template <int KIND, bool OPEN, int RPW>
+__global__ __launch_bounds__(2 * RPW) void duplex_kernel_wide(DuplexParams p) {
+    duplex_body<KIND, OPEN, RPW>(p);
+}
+
+template <int RPW>
+hipError_t launch_duplex_rpw(int kind, bool open, const DuplexParams& p, hipStream_t s) {
+    const uint32_t blocks = (p.n + RPW - 1) / RPW;
+    const dim3 g(blocks), b(2 * RPW);
+    switch (kind * 2 + (open ? 1 : 0)) {
+        case DK_FRAME * 2: hipLaunchKernelGGL((duplex_kernel<DK_FRAME, false, RPW>), g, b, 0, s, p); break;
+        case DK_FRAME * 2 + 1: hipLaunchKernelGGL((duplex_kernel<DK_FRAME, true, RPW>), g, b, 0, s, p); break;
+        case DK_CHUNK * 2: hipLaunchKernelGGL((duplex_kernel<DK_CHUNK, false, RPW>), g, b, 0, s, p); break;
+        case DK_CHUNK * 2 + 1: hipLaunchKernelGGL((duplex_kernel<DK_CHUNK, true, RPW>), g, b, 0, s, p); break;
+        case DK_AEADH * 2: hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, false, RPW>), g, b, 0, s, p); break;
+        case DK_AEADH * 2 + 1: hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, true, RPW>), g, b, 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s) {
-    const uint32_t blocks = (p.n + kDR - 1) / kDR;
-    if (blocks == 0) return hipSuccess;
-#define ENET_DX_LAUNCH(K, O) \
-    hipLaunchKernelGGL((duplex_kernel<K, O>), dim3(blocks), dim3(kDThreads), 0, s, p)
-    switch (kind * 2 + (open ? 1 : 0)) {
-        case DK_FRAME * 2: ENET_DX_LAUNCH(DK_FRAME, false); break;
-        case DK_FRAME * 2 + 1: ENET_DX_LAUNCH(DK_FRAME, true); break;
-        case DK_CHUNK * 2: ENET_DX_LAUNCH(DK_CHUNK, false); break;
-        case DK_CHUNK * 2 + 1: ENET_DX_LAUNCH(DK_CHUNK, true); break;
-        case DK_AEADH * 2:
-            hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, false>), dim3(blocks), dim3(kDThreads), 0, s, p);
-            break;
-        case DK_AEADH * 2 + 1:
-            hipLaunchKernelGGL((duplex_kernel_wide<DK_AEADH, true>), dim3(blocks), dim3(kDThreads), 0, s, p);
-            break;
-        default: return hipErrorInvalidValue;
-    }
-#undef ENET_DX_LAUNCH
-    return hipGetLastError();
+    if (p.n == 0) return hipSuccess;
+    static const int rpw_env = [] {
+        const char* e = std::getenv("ENET_DUPLEX_RPW");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    // Mixed lengths: 64-record workgroups, so the few long records (a workgroup lasts as long as
+    // its longest record's serial hash) occupy few SIMDs and the rest of the chip keeps pulling
+    // short workgroups (C5 device-resident: 88 -> 138 GiB/s).  Uniform batches: 256-record
+    // workgroups once there are >= 128 of them (C4 store 64 KiB: 230 vs 217 GiB/s), else 64.
+    const bool small = rpw_env ? rpw_env == 64 : (!p.uniform || p.n < 128u * 256u);
+    return small ? launch_duplex_rpw<64>(kind, open, p, s) : launch_duplex_rpw<256>(kind, open, p, s);
 }
 
 }  // namespace enet

@@ -111,6 +111,7 @@ struct DuplexParams {
     uint8_t* tags;             // AEADH seal: Poly1305 tags
     const uint8_t* tags_in;    // AEADH open: expected tags
     uint8_t* ok;               // open / fetch verdicts
+    int uniform;               // host hint: every record the same length (scheduling only)
 };
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s);
 

@@ -45,7 +45,7 @@ STALL_PASSES = [
 
 
 def kernel_key(name: str):
-    if "records_kernel" not in name and "sha_kernel" not in name and "stream_kernel" not in name:
+    if not any(k in name for k in ("records_kernel", "sha_kernel", "stream_kernel", "duplex_kernel")):
         return None
     return name.split("(")[0].replace("void ", "")
 
