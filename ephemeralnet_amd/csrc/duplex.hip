@@ -114,10 +114,29 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
     __syncthreads();
     const uint32_t Tmax = __builtin_amdgcn_readfirstlane(tmax_s);
 
-    const uint32_t msw = (lane >> 1) & 7u;  // 16-byte chunk swizzle of a 128-byte run in LDS
+    // 16-byte chunk swizzles (row = record rl): conflict-free ds_write_b128 (8-lane groups) and
+    // ds_read_b128 (16-lane groups) for the 128-byte runs and the 32-byte tail extension
+    const uint32_t msw = ((lane >> 1) & 7u) ^ ((lane & 1u) << 2);
+    const uint32_t xsw = ((lane >> 2) ^ (lane >> 3)) & 1u;
     uint8_t* const trow = ptb + (Tmax & 1u) * kBuf + rl * kRun;  // tail slot bytes 0..127
     uint8_t* const xrow = text + rl * 32u;                       // tail slot bytes 128..159
-    auto slot_byte = [&](uint32_t i) -> uint8_t* { return i < kRun ? trow + i : xrow + (i - kRun); };
+    auto slot_byte = [&](uint32_t i) -> uint8_t* {
+        return i < kRun ? trow + 16u * ((i >> 4) ^ msw) + (i & 15u)
+                        : xrow + 16u * (((i - kRun) >> 4) ^ xsw) + (i & 15u);
+    };
+    auto slot_put = [&](const uint32_t* w, int chunks) {  // slot words [0, 4 * chunks)
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            if (c < chunks) {
+                uint8_t* d = c < 8 ? trow + 16u * (c ^ msw) : xrow + 16u * ((c - 8) ^ xsw);
+                *reinterpret_cast<uint4*>(d) = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+            }
+        }
+    };
+    auto slot_chunk = [&](int c) -> uint4 {
+        const uint8_t* d = c < 8 ? trow + 16u * (c ^ msw) : xrow + 16u * ((c - 8) ^ xsw);
+        return *reinterpret_cast<const uint4*>(d);
+    };
 
     uint32_t kw[8];
     {
@@ -223,8 +242,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         if (!OPEN) {
             if (valid) {
                 // T1: the message tail to the hash lane
-#pragma unroll
-                for (int j = 0; j < 32; ++j) reinterpret_cast<uint32_t*>(trow)[j] = w[j];
+                slot_put(w, 8);
                 if (KIND != DK_FRAME && r) {
 #pragma unroll
                     for (int j = 0; j < 32; ++j) w[j] ^= ks[j];
@@ -249,9 +267,11 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 // T3: body tail = message tail || MAC, one run of body bytes
                 const uint32_t t = r + 32u;
 #pragma unroll
-                for (int j = 0; j < 32; ++j) w[j] = reinterpret_cast<const uint32_t*>(trow)[j] ^ ks[j];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) w[32 + j] = reinterpret_cast<const uint32_t*>(xrow)[j] ^ ks[32 + j];
+                for (int c = 0; c < 10; ++c) {
+                    const uint4 v = slot_chunk(c);
+                    w[4 * c] = v.x ^ ks[4 * c]; w[4 * c + 1] = v.y ^ ks[4 * c + 1];
+                    w[4 * c + 2] = v.z ^ ks[4 * c + 2]; w[4 * c + 3] = v.w ^ ks[4 * c + 3];
+                }
                 store_block(dst + tb, min(t, 64u), w);
                 if (t > 64u) store_block(dst + tb + 64, min(t - 64u, 64u), w + 16);
                 if (t > 128u) store_block(dst + tb + 128, t - 128u, w + 32);
@@ -281,13 +301,8 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                     store_block(dst + tb, min(r, 64u), w);
                     if (r > 64u) store_block(dst + tb + 64, r - 64u, w + 16);
                 }
-#pragma unroll
-                for (int j = 0; j < 32; ++j) reinterpret_cast<uint32_t*>(trow)[j] = w[j];
-                if (KIND == DK_FRAME) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) reinterpret_cast<uint32_t*>(xrow)[j] = w[32 + j];
-                }
-                if (KIND == DK_AEADH) xrow[31] = (uint8_t)aok;
+                slot_put(w, KIND == DK_FRAME ? 10 : 8);
+                if (KIND == DK_AEADH) *slot_byte(159) = (uint8_t)aok;
             }
             // the plaintext stores are complete before a hash lane may zero them on failure
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -333,10 +348,16 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 if ((uint32_t)k < nb) {
+                    uint32_t blk[16];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const uint4 v = k < 2 ? slot_chunk(4 * k + c) : make_uint4(0u, 0u, 0u, 0u);
+                        blk[4 * c] = v.x; blk[4 * c + 1] = v.y; blk[4 * c + 2] = v.z; blk[4 * c + 3] = v.w;
+                    }
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
                         const uint32_t b = 64u * k + 4u * i;
-                        const uint32_t v = k < 2 ? bswap32(reinterpret_cast<const uint32_t*>(trow)[16 * k + i]) : 0u;
+                        const uint32_t v = bswap32(blk[i]);
                         const uint32_t m = b + 4u <= r ? 0xffffffffu : (b >= r ? 0u : 0xffffffffu << (8u * (4u - (r - b))));
                         x[i] = (v & m) | ((r >> 2) == (b >> 2) ? 0x80000000u >> (8u * (r & 3u)) : 0u);
                     }
@@ -404,7 +425,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                     const uint8_t* ep = (KIND == DK_CHUNK ? p.expect : p.macs_in) + 32ull * rec;
 #pragma unroll
                     for (int j = 0; j < 8; ++j) diff |= ld32u(ep + 4 * j) ^ d[j];
-                    if (KIND == DK_AEADH && xrow[31] == 0) diff = 1;
+                    if (KIND == DK_AEADH && *slot_byte(159) == 0) diff = 1;
                 }
             }
             p.ok[rec] = diff == 0u ? 1 : 0;
