@@ -92,8 +92,9 @@ def main():
             out["eff_clock_ghz"] = m["GRBM_GUI_ACTIVE"] / 8.0 / m["dur_ns_p0"]
         if "GRBM_GUI_ACTIVE" in m and "SQ_ACTIVE_INST_VALU" in m:
             cyc = m["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
-            # ACTIVE_INST_VALU counts quad-cycles of VALU issue summed over SIMDs
-            out["valu_busy_frac"] = m["SQ_ACTIVE_INST_VALU"] * 4 / (cyc * 256 * 4)
+            # on gfx950 SQ_ACTIVE_INST_VALU equals SQ_INSTS_VALU (an instruction count summed over
+            # the 1024 SIMDs, not busy cycles): report kernel cycles per VALU instruction per SIMD
+            out["cycles_per_valu_instr_per_simd"] = cyc / (m["SQ_ACTIVE_INST_VALU"] / 1024.0)
             out["kernel_cycles"] = cyc
         if "TA_BUSY_avr" in m and "GRBM_GUI_ACTIVE" in m:
             out["ta_busy_frac"] = m["TA_BUSY_avr"] / (m["GRBM_GUI_ACTIVE"] / 8.0)
