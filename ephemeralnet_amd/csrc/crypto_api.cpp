@@ -22,6 +22,7 @@
 #include <random>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "enet_crypto.h"
 
@@ -35,21 +36,55 @@ void enet_check(int rc, const char* what) {
     if (rc != ENET_OK) throw std::runtime_error(std::string("enet: ") + what + ": " + enet_last_error());
 }
 
-// Grow-only device buffers + one stream per host thread: the reference functions are
-// reentrant and called from many session threads (SessionManager.cpp:332,703).
+// Staging buffers + one stream per host thread: the reference functions are reentrant and
+// called from many session threads (SessionManager.cpp:332,703).  A scalar call is a GPU round
+// trip, so its fixed cost is what matters: buffers of up to kZeroCopyMax bytes
+// come from one pinned, device-mapped, coherent host blob -- "uploading" is a host memcpy into
+// it, the kernel reads its operands over PCIe and writes its results straight back, and
+// "downloading" is a memcpy after the stream sync -- so a small call costs one launch and one
+// sync instead of up to six pageable copies.  Larger buffers keep grow-only device slots and
+// async copies.  The blob is bump-allocated and rewound at every sync (every API call ends
+// with one), so no region is rewritten while a kernel of the same call may still read it.
 struct Staging {
     static constexpr int kSlots = 10;
+    static constexpr size_t kHostBlob = 8u << 20;
+    static constexpr size_t kZeroCopyMax = 8u << 10;  // a serial SHA lane pays PCIe latency per block
     void* dev[kSlots] = {};
     size_t cap[kSlots] = {};
     hipStream_t stream = nullptr;
+    uint8_t* host = nullptr;
+    bool host_failed = false;
+    size_t used = 0;
+    struct Pending {
+        void* dst;
+        const void* src;
+        size_t n;
+    };
+    std::vector<Pending> pend;
 
     ~Staging() {
         for (int i = 0; i < kSlots; ++i)
             if (dev[i]) (void)hipFree(dev[i]);
+        if (host) (void)hipHostFree(host);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+    bool in_host(const void* p) const {
+        return host && p >= host && static_cast<const uint8_t*>(p) < host + kHostBlob;
     }
     void* get(int slot, size_t bytes) {
         bytes = std::max<size_t>(bytes, 64);
+        if (bytes <= kZeroCopyMax && !host_failed) {
+            if (!host && hipHostMalloc(reinterpret_cast<void**>(&host), kHostBlob,
+                                       hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+                host = nullptr;
+                host_failed = true;
+            }
+            const size_t off = (used + 255) & ~size_t(255);
+            if (host && off + bytes <= kHostBlob) {
+                used = off + bytes;
+                return host + off;
+            }
+        }
         if (cap[slot] < bytes) {
             if (dev[slot]) hip_check(hipFree(dev[slot]), "hipFree");
             size_t c = std::max(bytes, cap[slot] * 2);
@@ -63,12 +98,21 @@ struct Staging {
         return stream;
     }
     void h2d(void* d, const void* h, size_t n) {
-        if (n) hip_check(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s()), "H2D");
+        if (!n) return;
+        if (in_host(d)) std::memcpy(d, h, n);
+        else hip_check(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, s()), "H2D");
     }
     void d2h(void* h, const void* d, size_t n) {
-        if (n) hip_check(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s()), "D2H");
+        if (!n) return;
+        if (in_host(d)) pend.push_back({h, d, n});
+        else hip_check(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s()), "D2H");
     }
-    void sync() { hip_check(hipStreamSynchronize(s()), "hipStreamSynchronize"); }
+    void sync() {
+        hip_check(hipStreamSynchronize(s()), "hipStreamSynchronize");
+        for (const Pending& q : pend) std::memcpy(q.dst, q.src, q.n);
+        pend.clear();
+        used = 0;
+    }
 };
 
 Staging& staging() {
