@@ -255,6 +255,22 @@ def e2e(args) -> dict:
     }
 
 
+def dist_init(local: int):
+    """One process per GPU over nccl (= RCCL on ROCm).  ENET_BENCH_BACKEND=gloo rehearses the
+    N > 1 path on a one-GPU box: the ranks share cuda:(LOCAL_RANK mod device_count) and the
+    barrier / max-reduce run on the host.  Returns (device, device for the reduce tensor)."""
+    import torch
+    import torch.distributed as dist
+    backend = os.environ.get("ENET_BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+        return dev, dev
+    dist.init_process_group(backend)
+    return dev, torch.device("cpu")
+
+
 def c5(args) -> dict:
     """mixed log-uniform 512 B-64 KiB records with the fused HMAC-SHA256 tag,
     starting and ending in pinned host memory, through the library's host pipeline
@@ -270,10 +286,9 @@ def c5(args) -> dict:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = red_dev = torch.device("cuda", local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        dev, red_dev = dist_init(local)
     rng = np.random.default_rng(5)
     n_all = args.records * world
     lens_all = np.exp(rng.uniform(np.log(512), np.log(65536), n_all)).astype(np.int64)
@@ -294,7 +309,7 @@ def c5(args) -> dict:
     mx = int(lens.max()) if n else 0
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
-    pipe = E.Pipeline(local, args.c5_chunk_mib << 20, args.c5_streams)
+    pipe = E.Pipeline(dev.index, args.c5_chunk_mib << 20, args.c5_streams)
 
     def step():
         pipe.aead_hmac_seal(seal_b, ct_h, tags_h, macs_h)
@@ -309,7 +324,7 @@ def c5(args) -> dict:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     pipe.close()
@@ -400,10 +415,9 @@ def pow_bench(args) -> dict:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = red_dev = torch.device("cuda", local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        dev, red_dev = dist_init(local)
     n, A, sched = args.pow_jobs, args.pow_attempts, args.pow_schedule
     plen = 44 if sched == 1 else 88  # store prefix (empty hint) / handshake prefix
     g = torch.Generator(device=dev).manual_seed(77 + rank)
@@ -432,7 +446,7 @@ def pow_bench(args) -> dict:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -529,10 +543,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = red_dev = torch.device("cuda", local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        dev, red_dev = dist_init(local)
     E.lib()
     if args.lanes:
         E.set_lanes_per_record(args.lanes)
@@ -614,7 +627,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
