@@ -56,6 +56,11 @@ typedef struct enet_records {
                                    of the full batch, so results stay position-indexed. */
     uint64_t total_bytes_hint;  /* host-known sum of input lengths, 0 = unknown (scheduling) */
     uint32_t max_len_hint;      /* host-known max record length, 0 = unknown (scheduling) */
+    /* The hints only choose kernels and launch shapes.  total == count * max declares a uniform
+       batch (record i at in_offsets[0] + i * max); every workgroup of the uniform paths checks
+       its records' real offsets against that layout and takes the per-lane path over the real
+       offsets on any mismatch, so wrong hints cost speed, never bytes
+       (tests/test_gpu_parity.py::test_lying_hints_give_correct_bytes). */
 } enet_records;
 
 /* ---- ChaCha20 (reference: ChaCha20::apply, src/crypto/ChaCha20.cpp:98-121,
@@ -106,6 +111,8 @@ ENET_API int enet_hmac_sha256_verify_batch(uint32_t n, const uint8_t* keys, cons
  *       decrypted 32-byte MAC ([n][32] device buffer), ok[i] = MAC verified (records shorter
  *       than 32 bytes fail, Message.cpp:315); on failure out_i is zeroed.  The 16-byte wire
  *       header nonce || BE32(len) (SessionManager.cpp:376-387) is host framing. */
+/* One pass over HBM for any lengths / alignment / order (duplex kernel).  A record whose output
+ * length is not as stated is not processed: its output range is zeroed (and ok[i] = 0). */
 ENET_API int enet_frame_seal_batch(const enet_records* r, void* stream);
 ENET_API int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
 
@@ -122,7 +129,9 @@ ENET_API int enet_wire_seal_batch(const enet_records* r, void* stream);
 ENET_API int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
 
 /* ---- AEAD with a fused HMAC-SHA256 integrity tag ("AEAD plus fused
- *      HMAC-SHA256 tag and verify").  The HMAC covers the plaintext under the record's 32-byte
+ *      HMAC-SHA256 tag and verify"): ONE pass over HBM per direction (duplex kernel: Poly1305
+ *      in the cipher lanes, HMAC in the hash lanes on the same SIMDs).  in/out offsets
+ *      equal-length; mixed lengths are balanced best with `order` = longest first.  The HMAC covers the plaintext under the record's 32-byte
  *      key, exactly what the reference signs before encrypting (encode_signed,
  *      src/protocol/Message.cpp:305-311, HmacSha256.cpp:11-39).
  * seal: out_i = ChaCha20-Poly1305 ciphertext, tags[i] = Poly1305 tag, macs[i] = HMAC_K(pt_i).
@@ -142,8 +151,8 @@ ENET_API int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tag
  *        when chunk_ids == NULL (the daemon derives ids from content, ControlServer.cpp:1101).
  * fetch: out_i = ChaCha20(key_i, nonce_i, LE32(chunk_ids[i][0..3]), in_i); ok[i] =
  *        SHA-256(out_i) == chunk_hashes[i]; on mismatch out_i is zeroed (no plaintext).
- * Uniform batches (length a multiple of 128 B) with chunk_ids given take one fused pass over
- * HBM (hash and cipher together); content-derived ids need the digest first (two passes). */
+ * With chunk_ids given: one pass over HBM (hash and cipher together) for any lengths;
+ * content-derived ids need the digest first (two passes). */
 ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids,
                                     uint8_t* chunk_hashes, void* stream);
 ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
