@@ -117,6 +117,10 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         // launches this kernel only for arenas < 4 GiB.
         const uint32_t m = wave - 8u;
         const uint32_t kk = lane & 7u;
+        // the memory waves win issue arbitration: their one instruction per keystream barrier
+        // interval then never waits behind the compute waves' VALU stream (C2: +1-2 %,
+        // tools/prio_ab.sh 876/879/889 -> 893/896/899 GiB/s on one box)
+        if (!(dbg & 4096)) __builtin_amdgcn_s_setprio(3);
         uint32_t offA[2], offAB[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
