@@ -147,6 +147,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
 
     if (cipher) {
         // ============================================================== cipher lane
+        if (p.prio == 2) __builtin_amdgcn_s_setprio(2);
         const uint8_t* src = p.in + ib + (OPEN ? H : 0u);
         uint8_t* dst = p.out + ob + (OPEN ? 0u : H);
         const uint32_t off0 = OPEN ? H : 0u;  // offset of src inside the input record
@@ -310,6 +311,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         }
     } else {
         // ============================================================== hash lane
+        if (p.prio == 1) __builtin_amdgcn_s_setprio(2);
         // frames / AEAD: HMAC-SHA256 (HmacSha256.cpp:11-39) with the 32-byte record key;
         // chunks: SHA-256 (Sha256::digest, Sha256.cpp:66-132)
         uint32_t kb[8];
@@ -464,6 +466,12 @@ hipError_t launch_duplex_rpw(int kind, bool open, const DuplexParams& p, hipStre
 
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
+    static const int prio_env = [] {
+        const char* e = std::getenv("ENET_DUPLEX_PRIO");
+        return e ? (int)std::strtol(e, nullptr, 10) : 0;
+    }();
+    DuplexParams q = p;
+    q.prio = prio_env;
     static const int rpw_env = [] {
         const char* e = std::getenv("ENET_DUPLEX_RPW");
         return e ? (int)std::strtol(e, nullptr, 10) : 0;
@@ -473,7 +481,7 @@ hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t
     // short workgroups (C5 device-resident: 88 -> 138 GiB/s).  Uniform batches: 256-record
     // workgroups once there are >= 128 of them (C4 store 64 KiB: 230 vs 217 GiB/s), else 64.
     const bool small = rpw_env ? rpw_env == 64 : (!p.uniform || p.n < 128u * 256u);
-    return small ? launch_duplex_rpw<64>(kind, open, p, s) : launch_duplex_rpw<256>(kind, open, p, s);
+    return small ? launch_duplex_rpw<64>(kind, open, q, s) : launch_duplex_rpw<256>(kind, open, q, s);
 }
 
 }  // namespace enet

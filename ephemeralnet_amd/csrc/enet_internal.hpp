@@ -112,6 +112,7 @@ struct DuplexParams {
     const uint8_t* tags_in;    // AEADH open: expected tags
     uint8_t* ok;               // open / fetch verdicts
     int uniform;               // host hint: every record the same length (scheduling only)
+    int prio;                  // issue priority: 1 = hash waves first, 2 = cipher waves first
 };
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s);
 
