@@ -483,7 +483,9 @@ def test_wire_frames_random_vs_oracle(enet, lanes):
                                        (640, 700, 1), (127, 300, 1), (64, 260, 1), (0, 10, 1),
                                        (1504, 300, 1), (1472, 300, 1), (1400, 300, 1),
                                        (200, 300, 1), (100, 260, 1), (80, 300, 1), (31, 300, 1),
-                                       (17, 300, 1), (16, 300, 1), (15, 300, 1), (143, 300, 1)])
+                                       (17, 300, 1), (16, 300, 1), (15, 300, 1), (143, 300, 1),
+                                       (132, 600, 1), (196, 600, 1), (192, 520, 1), (1000, 600, 1),
+                                       (4100, 520, 1)])
 def test_aead_uniform_batches_vs_oracle(enet, L, n, lanes, staging):
     """Uniform-length batches take the cooperative LDS-staged path (whole workgroups; staging
     variant 1 = register prefetch, 3 = LDS DMA) plus the per-lane path for the partial
