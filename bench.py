@@ -760,8 +760,10 @@ def main():
                 "traffic": traffic,
                 "traffic_source": pmc_note,
                 "algorithmic_bytes_per_launch": seal_bytes if dom == "seal" else open_bytes,
-                "note": "VALU-bound (ChaCha20 ARX + Poly1305 limb products) with HBM traffic of the "
-                        "same order: see valu_roofline",
+                "note": "power-capped: with the keystream and HBM streaming together the package sits "
+                        "at ~1.38 kW and the shader clock drops to ~2.08 GHz (2.39 GHz with either alone); "
+                        "in shader cycles the kernel is within 5 % of its compute-only form "
+                        "(profiles/r02_power.txt); VALU work: see valu_roofline",
             },
             "valu_roofline": valu,
         }

@@ -88,6 +88,15 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     const uint32_t gid = blockIdx.x * kStreamLanes + (compute ? threadIdx.x : 0u);
     const uint32_t rec = gid >> LOGP;  // the launch covers records [0, n), n = whole workgroups
     const uint32_t j = gid & (P - 1);
+    // probe (dbg 16384, tools/stage_probe.py): compute wave 0 stamps the 100 MHz clock and the
+    // shader clock at entry, the shader clock at the body start, after every stage barrier S0 and
+    // after F1, and both clocks at exit, into the workgroup's tag slots
+    const bool stamp = (p.dbg & 16384) && threadIdx.x == 0 && p.tag_out;
+    uint64_t* stamps = reinterpret_cast<uint64_t*>(p.tag_out + 16ull * rec);
+    if (__builtin_expect(stamp, 0)) {
+        stamps[0] = __builtin_amdgcn_s_memrealtime();
+        stamps[1] = __builtin_amdgcn_s_memtime();
+    }
     const uint64_t i0 = p.in_off[0], o0 = p.out_off[0];
     {
         const bool mine = !compute || (p.in_off[rec] == i0 + (uint64_t)rec * L &&
@@ -144,8 +153,15 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
 #pragma unroll
         for (int s = 0; s < 16; ++s)
             offs[s] = offA[s >> 3] + (uint32_t)(s & 1) * offAB[s >> 3] + (uint32_t)((s & 7) >> 1) * offD;
-        const uint8_t* ibase = p.in + i0;
-        uint8_t* obase = p.out + o0;
+        // the arena bases are SGPR operands of the DMA / store asm: keep them provably uniform
+        auto uni = [](const void* q) {
+            const uint64_t v = reinterpret_cast<uintptr_t>(q);
+            // (readfirstlane returns int: zero-extend, a sign-extended low half corrupts the address)
+            return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+        };
+        const uint8_t* ibase = reinterpret_cast<const uint8_t*>(uni(p.in + i0));
+        uint8_t* obase = reinterpret_cast<uint8_t*>(uni(p.out + o0));
         // this wave's parts of the slabs: compute waves 2m and 2m+1, adjacent
         const uint32_t in_part = (uint32_t)reinterpret_cast<uintptr_t>(s_in) + 2u * m * (64u * kRun);
         const uint8_t* out_part = s_out + 2u * m * (64u * kRun) + 16u * lane;
@@ -223,6 +239,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
 
     // ==================================================================== compute waves
     const uint32_t msw = slab_sw(lane);
+    if (__builtin_expect(stamp, 0)) stamps[2] = __builtin_amdgcn_s_memtime();
 
     // ---- per-record ChaCha20 constants
     uint32_t kw[8], nw[3];
@@ -287,6 +304,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         // S0(st): the memory waves saw stage st land; this wave's output writes are done
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         stream_barrier();
+        if (__builtin_expect(stamp, 0)) stamps[3 + st] = __builtin_amdgcn_s_memtime();
         uint8_t* myrun = s_in + threadIdx.x * kRun;
         // the run is read now and consumed after the keystream, so its LDS latency is hidden
         uint32_t w[32];
@@ -361,14 +379,19 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     stream_barrier();  // F1
+    if (__builtin_expect(stamp, 0)) stamps[3 + S] = __builtin_amdgcn_s_memtime();
 
-    if (dbg & (256 | 2048)) {  // 4 words at the workgroup's first tag slot: clk0, rt0, clk1, rt1
+    if (dbg & (256 | 2048 | 16384)) {  // 4 words at the workgroup's first tag slot: clk0, rt0, clk1, rt1
         const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-        if (threadIdx.x == 0 && p.tag_out && !(dbg & 2048)) {
+        if (threadIdx.x == 0 && p.tag_out && !(dbg & (2048 | 16384))) {
             uint64_t* d = reinterpret_cast<uint64_t*>(p.tag_out + 16ull * rec);
             d[0] = clk0; d[1] = rt0; d[2] = clk1; d[3] = rt1;
         }
         stream_barrier();  // F2
+        if (__builtin_expect(stamp, 0)) {
+            stamps[4 + S] = __builtin_amdgcn_s_memtime();
+            stamps[5 + S] = __builtin_amdgcn_s_memrealtime();
+        }
         return;
     }
     uint32_t diff = 0;
