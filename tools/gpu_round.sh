@@ -2,13 +2,16 @@
 # One GPU session producing the round's evidence under gpurun_out/r$R/: GPU parity suite, the
 # default bench line, side configs/modes, the torchrun launch path, rocprofv3 kernel stats, and
 # PMC passes (C2 and C3).
-# usage (on the box, from the repo root): bash tools/gpu_round.sh 01
+# usage (on the box, from the repo root): bash tools/gpu_round.sh 01 [a|b|all]
+# (a = parity suite, bench lines and side configs; b = rocprof stats and PMC: two gpurun calls)
 set -euo pipefail
 R=${1:-01}
+PART=${2:-all}
 O=gpurun_out/r$R
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "[$(date +%T)] $*"; }
+if [ "$PART" != b ]; then
 step pytest
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 tail -2 $O/pytest_gpu.log
@@ -28,6 +31,8 @@ for args in "--records 1048576 --record-bytes 1500" "--records 32768 --record-by
   step "  $args"
   timeout -k 10 240 python bench.py --steps 100 --warmup 20 $(case "$args" in *pow*|*1048576*|*c5-device*|*32768*) echo "--steps 10 --warmup 3";; esac) $(case "$args" in *pow*|*wire*) ;; *) echo --no-cpu-baseline;; esac) $args >> $O/side.jsonl 2>> $O/side.err
 done
+fi
+if [ "$PART" != a ]; then
 step rocprof stats
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 > $O/prof_bench.json 2> $O/prof.err
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3.json 2>> $O/prof.err
@@ -38,4 +43,5 @@ find $O/prof $O/prof_c3 $O/prof_fused $O/prof_c3w $O/prof_c5 -name "*stats*"
 step pmc
 timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc.log 2>&1
 timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3 --summary $O/pmc_c3_summary.json --config "{\"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3.log 2>&1
+fi
 step done
