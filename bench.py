@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--record-bytes", type=int, default=4096)
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per record (0 = scheduler)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-power", action="store_true",
+                    help="skip the rocm-smi package power / sclk sample after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="approximate wall budget of the CPU baseline sample")
     ap.add_argument("--e2e", action="store_true",
@@ -253,6 +255,48 @@ def e2e(args) -> dict:
                    "streams": args.streams, "host_buffers": "pinned",
                    "path": "enet_pipeline_aead_seal/open (libenet_crypto.so)"},
     }
+
+
+def sample_power(step, sync, secs: float = 2.5) -> dict | None:
+    """Package power and shader clock while the step runs back to back (after the timed region):
+    rocm-smi in a child process samples a few times, the busiest GPU's readings are reported
+    (the kernels are power-capped, DESIGN.md 4 / profiles/r02_power.txt).  None if rocm-smi is
+    unavailable."""
+    import re
+    import subprocess
+    import statistics
+    cmd = "sleep 0.8; for i in 1 2 3; do rocm-smi --showpower --showclocks; sleep 0.3; done"
+    try:
+        proc = subprocess.Popen(["bash", "-c", cmd], stdout=subprocess.PIPE,
+                                stderr=subprocess.DEVNULL, text=True)
+    except OSError:
+        return None
+    t0 = time.perf_counter()
+    while proc.poll() is None and time.perf_counter() - t0 < secs + 4:
+        for _ in range(8):
+            step()
+        sync()
+    try:
+        txt = proc.communicate(timeout=5)[0]
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        return None
+    pw, clk = {}, {}
+    for line in txt.splitlines():
+        m = re.search(r"GPU\[(\d+)\].*Package Power \(W\):\s*([0-9.]+)", line)
+        if m:
+            pw.setdefault(int(m.group(1)), []).append(float(m.group(2)))
+        m = re.search(r"GPU\[(\d+)\].*sclk clock level:.*\((\d+)Mhz\)", line)
+        if m:
+            clk.setdefault(int(m.group(1)), []).append(float(m.group(2)))
+    if not pw:
+        return None
+    g = max(pw, key=lambda k: statistics.median(pw[k]))
+    return {"package_w": statistics.median(pw[g]),
+            "sclk_mhz": statistics.median(clk[g]) if g in clk else None,
+            "samples": len(pw[g]),
+            "source": "rocm-smi while seal/open pairs run back to back after the timed region "
+                      "(busiest GPU); idle sclk 2.4 GHz, package cap ~1.4 kW"}
 
 
 def dist_init(local: int):
@@ -660,6 +704,9 @@ def main():
         raise SystemExit(f"rank {rank}: open(seal(x)) != x")
     if args.mode in ("aead", "xor", "store") and torch.equal(ct, pt):
         raise SystemExit(f"rank {rank}: ciphertext equals plaintext")
+    power = None
+    if world == 1 and not args.no_power and args.mode in ("aead", "xor"):
+        power = sample_power(lambda: (seal(), open_()), lambda: torch.cuda.synchronize(dev))
 
     if rank == 0:
         total_bytes = n * L * args.steps * world
@@ -767,6 +814,8 @@ def main():
             },
             "valu_roofline": valu,
         }
+        if power:
+            out["power"] = power
         if not args.no_cpu_baseline and world == 1:
             if args.mode == "wire":  # the same workload through the reference itself
                 ref = cpu_reference_frames(L, args.cpu_seconds)
