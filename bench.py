@@ -273,7 +273,7 @@ def sample_power(step, sync, secs: float = 2.5) -> dict | None:
         return None
     t0 = time.perf_counter()
     while proc.poll() is None and time.perf_counter() - t0 < secs + 4:
-        for _ in range(8):
+        for _ in range(64):  # ~18 ms of queued work per host sync: no idle gaps in the sample
             step()
         sync()
     try:
