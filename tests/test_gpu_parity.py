@@ -768,3 +768,53 @@ def test_aead_uniform_out_arena_phase(enet, shift):
     for i in range(0, n, 7):
         ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
         assert got[i] == ct and th[16 * i:16 * i + 16] == tag, i
+
+
+@pytest.mark.parametrize("ishift,oshift", [(4, 4), (8, 100), (0, 12), (64, 0)])
+def test_stream_kernel_unaligned_arenas(enet, ishift, oshift):
+    """The headline streaming kernel (C2 shape: 4 KiB records, two lanes each, whole 512-lane
+    workgroups) with input / output arenas that start off 16-byte alignment: its LDS DMAs and
+    whole-run stores then take unaligned 16-byte pieces.  Bit-exact against the oracle (seal and
+    the reference-mode ChaCha20), open(seal(x)) == x, and a tampered record rejected and zeroed."""
+    import torch
+    enet.set_lanes_per_record(2)
+    enet.set_staging(-1)
+    n, L = 768, 4096
+    items = [splitmix_bytes(91000 + i, L) for i in range(n)]
+    keys = [splitmix_bytes(92000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(93000 + i, 12) for i in range(n)]
+    b0 = enet.make_batch(items, keys, nonces)
+    ibig = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    ibig[ishift:ishift + n * L] = b0.arena
+    src = ibig[ishift:ishift + n * L]
+    b = enet.Batch(src, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    obig = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    out = obig[oshift:oshift + n * L]
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    offs = b0.offsets.cpu().tolist()
+    got, th = records_of(host(out), offs), host(tags)
+    for i in list(range(0, n, 37)) + [n - 1]:
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct and th[16 * i:16 * i + 16] == tag, i
+    assert int(obig[:oshift].count_nonzero()) == 0 and int(obig[oshift + n * L:].count_nonzero()) == 0
+    b2 = enet.Batch(out, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    bbig = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    back = bbig[ishift:ishift + n * L]
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, back, tags, ok)
+    assert int(ok.sum()) == n and torch.equal(back, src)
+    bad = out.clone()
+    bad[offs[300] + 2049] ^= 4
+    b3 = enet.Batch(bad, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    enet.aead_open(b3, back, tags, ok)
+    okh = ok.cpu().tolist()
+    assert okh[300] == 0 and sum(okh) == n - 1
+    bh = records_of(host(back), offs)
+    assert bh[300] == bytes(L) and bh[299] == items[299] and bh[301] == items[301]
+    xo = obig[oshift:oshift + n * L]
+    enet.chacha20_xor(b, xo)
+    xg = records_of(host(xo), offs)
+    for i in range(0, n, 97):
+        assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], 0), i
+    enet.set_lanes_per_record(0)
