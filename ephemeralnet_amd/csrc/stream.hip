@@ -173,8 +173,14 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         auto dma = [&](const uint8_t* base, int s) {
             const uint32_t m0 = in_part + 1024u * (uint32_t)s;
             uint32_t keep;
-            asm volatile("s_mov_b32 %0, m0\n s_mov_b32 m0, %2\n s_nop 0\n global_load_lds_dwordx4 %1, %3\n s_mov_b32 m0, %0"
-                         : "=&s"(keep) : "v"(offs[s]), "s"(m0), "s"(base) : "memory");
+            // non-temporal: every input line is read exactly once (C2: +1.2 %, three interleaved
+            // pairs, tools/stagger_ab.sh "0 14"; SCHED 14 = plain loads for the A/B)
+            if constexpr (SCHED == 14)
+                asm volatile("s_mov_b32 %0, m0\n s_mov_b32 m0, %2\n s_nop 0\n global_load_lds_dwordx4 %1, %3\n s_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(offs[s]), "s"(m0), "s"(base) : "memory");
+            else
+                asm volatile("s_mov_b32 %0, m0\n s_mov_b32 m0, %2\n s_nop 0\n global_load_lds_dwordx4 %1, %3 nt\n s_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(offs[s]), "s"(m0), "s"(base) : "memory");
         };
         auto ldsread = [&](int s) {
             return *reinterpret_cast<const uint4*>(out_part + 1024u * (uint32_t)s);
@@ -450,6 +456,7 @@ static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_
                 case 3: hipLaunchKernelGGL((stream_kernel<1, MODE, 3>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 4: hipLaunchKernelGGL((stream_kernel<1, MODE, 4>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 5: hipLaunchKernelGGL((stream_kernel<1, MODE, 5>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
+                case 14: hipLaunchKernelGGL((stream_kernel<1, MODE, 14>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 default: hipLaunchKernelGGL((stream_kernel<1, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
             }
             break;
