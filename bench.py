@@ -257,18 +257,35 @@ def e2e(args) -> dict:
     }
 
 
-def sample_power(step, sync, secs: float = 2.5) -> dict | None:
+def under_profiler() -> bool:
+    """rocprofv3 preloads its library (and initialises the GPU) before the program starts."""
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+
+
+def start_power_sampler():
+    """Fork the rocm-smi sampler BEFORE this process touches the GPU: the child waits on its stdin,
+    then runs rocm-smi three times; this process never starts a program after GPU initialisation.
+    None when unwanted (N > 1, --no-power, other modes, under a profiler) or unavailable."""
+    import subprocess
+    cmd = "read go || exit 0; sleep 0.8; for i in 1 2 3; do rocm-smi --showpower --showclocks; sleep 0.3; done"
+    try:
+        return subprocess.Popen(["bash", "-c", cmd], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                stderr=subprocess.DEVNULL, text=True)
+    except OSError:
+        return None
+
+
+def sample_power(proc, step, sync, secs: float = 2.5) -> dict | None:
     """Package power and shader clock while the step runs back to back (after the timed region):
-    rocm-smi in a child process samples a few times, the busiest GPU's readings are reported
-    (the kernels are power-capped, DESIGN.md 4 / profiles/r02_power.txt).  None if rocm-smi is
-    unavailable."""
+    the pre-forked sampler (start_power_sampler) reads rocm-smi a few times, the busiest GPU's
+    readings are reported (the kernels are power-capped, DESIGN.md 4 / profiles/r02_power.txt)."""
     import re
     import subprocess
     import statistics
-    cmd = "sleep 0.8; for i in 1 2 3; do rocm-smi --showpower --showclocks; sleep 0.3; done"
     try:
-        proc = subprocess.Popen(["bash", "-c", cmd], stdout=subprocess.PIPE,
-                                stderr=subprocess.DEVNULL, text=True)
+        proc.stdin.write("go\n")
+        proc.stdin.flush()
     except OSError:
         return None
     t0 = time.perf_counter()
@@ -579,6 +596,10 @@ def main():
     if args.e2e:
         print(json.dumps(e2e(args)), flush=True)
         return
+    sampler = None
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_power
+            and args.mode in ("aead", "xor") and not under_profiler()):
+        sampler = start_power_sampler()  # before any GPU initialisation in this process
     import torch
     import torch.distributed as dist
 
@@ -705,8 +726,8 @@ def main():
     if args.mode in ("aead", "xor", "store") and torch.equal(ct, pt):
         raise SystemExit(f"rank {rank}: ciphertext equals plaintext")
     power = None
-    if world == 1 and not args.no_power and args.mode in ("aead", "xor"):
-        power = sample_power(lambda: (seal(), open_()), lambda: torch.cuda.synchronize(dev))
+    if sampler is not None:
+        power = sample_power(sampler, lambda: (seal(), open_()), lambda: torch.cuda.synchronize(dev))
 
     if rank == 0:
         total_bytes = n * L * args.steps * world

@@ -34,14 +34,14 @@ done
 fi
 if [ "$PART" != a ]; then
 step rocprof stats
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --steps 50 --warmup 10 > $O/prof_bench.json 2> $O/prof.err
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3.json 2>> $O/prof.err
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fused -o fused -- python3 bench.py --no-cpu-baseline --mode store --steps 20 --warmup 5 > $O/prof_fused.json 2>> $O/prof.err
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3w -o c3w -- python3 bench.py --no-cpu-baseline --mode wire --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3w.json 2>> $O/prof.err
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --c5-device --records 65536 --steps 5 --warmup 2 > $O/prof_c5.json 2>> $O/prof.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py --no-cpu-baseline --no-power --steps 50 --warmup 10 > $O/prof_bench.json 2> $O/prof.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3 -o c3 -- python3 bench.py --no-cpu-baseline --no-power --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3.json 2>> $O/prof.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_fused -o fused -- python3 bench.py --no-cpu-baseline --no-power --mode store --steps 20 --warmup 5 > $O/prof_fused.json 2>> $O/prof.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c3w -o c3w -- python3 bench.py --no-cpu-baseline --no-power --mode wire --records 1048576 --record-bytes 1500 --steps 10 --warmup 3 > $O/prof_c3w.json 2>> $O/prof.err
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_c5 -o c5 -- python3 bench.py --no-power --c5-device --records 65536 --steps 5 --warmup 2 > $O/prof_c5.json 2>> $O/prof.err
 find $O/prof $O/prof_c3 $O/prof_fused $O/prof_c3w $O/prof_c5 -name "*stats*"
 step pmc
-timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc.log 2>&1
-timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3 --summary $O/pmc_c3_summary.json --config "{\"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3.log 2>&1
+timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --no-power --steps 3 --warmup 1 > $O/pmc.log 2>&1
+timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3 --summary $O/pmc_c3_summary.json --config "{\"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --no-power --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3.log 2>&1
 fi
 step done
