@@ -18,6 +18,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -98,23 +99,48 @@ def parse():
     return ap.parse_args()
 
 
+def host_threads() -> int:
+    """Threads for the CPU baselines: every core in this process's affinity mask (BASELINE.md 3 /
+    SURVEY 8d: all host cores, the count stated in the line)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        return max(1, os.cpu_count() or 1)
+
+
+def host_cpu_info() -> dict:
+    """nproc, the affinity mask size, the lscpu model name and the cgroup CPU quota (cpu.max),
+    recorded beside every CPU number so the baseline's hardware is explicit."""
+    info = {"nproc": os.cpu_count(), "affinity": host_threads(), "model": None, "cgroup_cpu_max": None}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                info["model"] = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            info["cgroup_cpu_max"] = f.read().strip()
+    except OSError:
+        pass
+    return info
+
+
 def cpu_baseline(record_bytes: int, budget_s: float) -> dict:
     """The CPU oracle (oracle/enet_oracle.c: byte-wise ChaCha20 like src/crypto/ChaCha20.cpp,
     RFC 8439 Poly1305) on a bounded sample of the same workload, all host threads of this rank's
-    share (<= 16), same metric: sum L / (t_seal + t_open)."""
+    affinity mask (every core this rank may run on), same metric: sum L / (t_seal + t_open)."""
     import ctypes as C
 
     import numpy as np
 
     import oracle
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    threads = host_threads()
     L = record_bytes
-    n = 512 * threads
+    n = max(512 * 16, 64 * threads)
     rng = np.random.default_rng(1)
     pt = rng.integers(0, 256, n * L, dtype=np.uint8)
     keys = rng.integers(0, 256, n * 32, dtype=np.uint8)
@@ -148,6 +174,7 @@ def cpu_baseline(record_bytes: int, budget_s: float) -> dict:
         "unit": "GiB/s",
         "cores": threads,
         "one_core_value": round(one_core, 4),
+        "host": host_cpu_info(),
         "kind": "port",
         "sample": f"{reps} x {n} records x {L} B AEAD seal+open (oracle/enet_oracle.c, "
                   f"byte-wise like src/crypto/ChaCha20.cpp, -O2), {threads} threads",
@@ -181,13 +208,9 @@ def cpu_reference_frames(record_bytes: int, budget_s: float) -> dict | None:
     lib = ref_lib()
     if lib is None:
         return None
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
+    threads = host_threads()
     L = record_bytes
-    n = 128 * threads
+    n = max(128 * 16, 16 * threads)
     rng = np.random.default_rng(3)
     pt = rng.integers(0, 256, n * L, dtype=np.uint8)
     keys = rng.integers(0, 256, n * 32, dtype=np.uint8)
@@ -204,7 +227,7 @@ def cpu_reference_frames(record_bytes: int, budget_s: float) -> dict | None:
         if time.perf_counter() - t_start > budget_s or reps >= 64:
             break
     return {"value": round(reps * n * L / total_s / 2**30, 4), "unit": "GiB/s", "cores": threads,
-            "kind": "reference",
+            "host": host_cpu_info(), "kind": "reference",
             "sample": f"{reps} x {n} records x {L} B, reference frame seal+open (HMAC-SHA256 + "
                       f"ChaCha20, oracle/_ref compiled from src/crypto), {threads} threads"}
 
@@ -546,7 +569,7 @@ def pow_bench(args) -> dict:
         if not args.no_cpu_baseline and world == 1:
             import ctypes as C
 
-            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+            threads = host_threads()
             m = 64 * threads
             cpu_att = max(256, int(args.cpu_seconds * 2e6 / m))  # ~2 M hashes/s per thread budget
             lib = ref_lib() if sched == 1 else None
@@ -570,7 +593,7 @@ def pow_bench(args) -> dict:
                                       "src/crypto/Sha256.cpp, -O2")
             out["cpu_baseline"] = {
                 "value": round(hashes / secs / 1e9, 5), "unit": "G candidates/s", "cores": threads,
-                "kind": kind,
+                "host": host_cpu_info(), "kind": kind,
                 "sample": f"{m} {'store' if sched else 'handshake'}-PoW jobs x {cpu_att} attempts at "
                           f"difficulty 24 ({what})"}
     if world > 1:

@@ -13,8 +13,13 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libenet_crypto.so")
 OBJ = os.path.join(PKG, "build")
-SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "capi.cpp", "crypto_api.cpp", "pipeline.cpp"]
-HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp"]
+# tools build: the same sources with -DENET_TOOLS_BUILD (stream-kernel probes and schedule
+# variants selectable from the environment); loaded only through ENET_LIB_PATH by tools/
+LIB_TOOLS = os.path.join(PKG, "libenet_crypto_tools.so")
+OBJ_TOOLS = os.path.join(PKG, "build_tools")
+SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "capi.cpp", "crypto_api.cpp",
+           "pipeline.cpp", "host_engine.cpp"]
+HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "host_engine.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC",
           "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
@@ -22,52 +27,66 @@ CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC",
 LDFLAGS = ["--offload-arch=gfx950", "-fPIC", "-shared"]
 
 
-def _headers() -> list[str]:
-    deps = [os.path.join(CSRC, f) for f in HEADERS]
+DEVICE_HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "chacha_lockstep_asm.hpp"]
+
+
+def _headers(src: str = "") -> list[str]:
+    """Headers a source depends on: kernels (.hip) only the device headers; host C++ (.cpp) those,
+    the host engine's and everything under include/."""
+    if src.endswith(".hip"):
+        return [os.path.join(CSRC, f) for f in DEVICE_HEADERS if os.path.exists(os.path.join(CSRC, f))]
+    deps = [os.path.join(CSRC, f) for f in HEADERS + ["chacha_lockstep_asm.hpp"]]
     for dp, _, fs in os.walk(os.path.join(ROOT, "include")):
         deps += [os.path.join(dp, f) for f in fs]
     return [d for d in deps if os.path.exists(d)]
 
 
-def _obj(src: str) -> str:
-    return os.path.join(OBJ, os.path.splitext(src)[0] + ".o")
+def _hdr_time(src: str) -> float:
+    return max((os.path.getmtime(h) for h in _headers(src)), default=0.0)
 
 
-def _stale_obj(src: str, hdr_t: float) -> bool:
-    o = _obj(src)
+def _obj(src: str, obj_dir: str = OBJ) -> str:
+    return os.path.join(obj_dir, os.path.splitext(src)[0] + ".o")
+
+
+def _stale_obj(src: str, hdr_t: float, obj_dir: str = OBJ) -> bool:
+    o = _obj(src, obj_dir)
     if not os.path.exists(o):
         return True
     t = os.path.getmtime(o)
     return os.path.getmtime(os.path.join(CSRC, src)) > t or hdr_t > t
 
 
-def build(force: bool = False, verbose: bool = True, jobs: int | None = None) -> str:
-    os.makedirs(OBJ, exist_ok=True)
-    hdr_t = max((os.path.getmtime(h) for h in _headers()), default=0.0)
-    todo = [s for s in SOURCES if force or _stale_obj(s, hdr_t)]
-    if not todo and os.path.exists(LIB) and \
-            os.path.getmtime(LIB) >= max(os.path.getmtime(_obj(s)) for s in SOURCES):
-        return LIB
+def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
+          tools: bool = False) -> str:
+    obj_dir, lib = (OBJ_TOOLS, LIB_TOOLS) if tools else (OBJ, LIB)
+    cflags = CFLAGS + (["-DENET_TOOLS_BUILD"] if tools else [])
+    os.makedirs(obj_dir, exist_ok=True)
+    todo = [s for s in SOURCES if force or _stale_obj(s, _hdr_time(s), obj_dir)]
+    if not todo and os.path.exists(lib) and \
+            os.path.getmtime(lib) >= max(os.path.getmtime(_obj(s, obj_dir)) for s in SOURCES):
+        return lib
 
     def cc(src: str) -> None:
-        cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", _obj(src) + ".tmp"]
+        o = _obj(src, obj_dir)
+        cmd = [HIPCC] + cflags + ["-c", os.path.join(CSRC, src), "-o", o + ".tmp"]
         if verbose:
             print("[build]", " ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        os.replace(_obj(src) + ".tmp", _obj(src))
+        os.replace(o + ".tmp", o)
 
     n = jobs or min(len(todo) or 1, max(1, min(8, os.cpu_count() or 1)))
     with ThreadPoolExecutor(max_workers=n) as ex:
         for f in [ex.submit(cc, s) for s in todo]:
             f.result()
-    tmp = LIB + ".tmp"
-    cmd = [HIPCC] + LDFLAGS + [_obj(s) for s in SOURCES] + ["-o", tmp]
+    tmp = lib + ".tmp"
+    cmd = [HIPCC] + LDFLAGS + [_obj(s, obj_dir) for s in SOURCES] + ["-o", tmp]
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, tools="--tools" in sys.argv)

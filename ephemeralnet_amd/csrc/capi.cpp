@@ -93,6 +93,12 @@ enet::RecParams rec_params(const enet_records* r) {
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.stream = dflt ? strm : 0;
+#ifdef ENET_TOOLS_BUILD
+    // Measurement probes of the stream kernel (skip keystream / Poly1305 / stores, clock stamps in
+    // tag_out) and its memory-schedule variants.  Only the tools build of the library
+    // (build.py --tools -> libenet_crypto_tools.so, loaded via ENET_LIB_PATH) reads them: a
+    // probe produces wrong ciphertext and tags by design, so the shipping library cannot be
+    // switched into one from the environment.
     static const int dbg = [] {
         const char* e = std::getenv("ENET_STREAM_DBG");
         return e ? (int)std::strtol(e, nullptr, 10) : 0;
@@ -103,6 +109,7 @@ enet::RecParams rec_params(const enet_records* r) {
         return e ? (int)std::strtol(e, nullptr, 10) : 0;
     }();
     p.var = var;
+#endif
 
     if (p.coop == 4) p.coop = 1;
     // COOP 3 addresses the arena with 32-bit offsets

@@ -1,7 +1,17 @@
-// crypto_api.cpp -- the reference C++ API (namespace ephemeralnet::crypto) implemented on the
-// MI355X through the C ABI.  Every call ships its record(s) to the device, runs the batch
-// kernels and copies the result back; there is no CPU crypto path in the product (a failing
-// GPU path throws std::runtime_error instead of silently computing on the host).
+// crypto_api.cpp -- the reference C++ API (namespace ephemeralnet::crypto, security, network)
+// implemented over the C ABI and the scalar host engine.
+//
+// Two kinds of entry points live here:
+//   * the reference's own signatures (ChaCha20::apply, Sha256, HmacSha256, CryptoManager,
+//     security::*, network::KeyManager): one record per call, from many session threads, never
+//     throwing.  They are routed by size (enet_crypto.h "scalar"): serial and
+//     small work on the calling thread's host engine (host_engine.cpp), large ChaCha20 records
+//     on the MI355X with concurrent callers coalesced into one launch, PoW searches on the
+//     MI355X.  A device failure finishes the call on the host engine (bit-exact) instead of
+//     throwing into a caller that never catches (SessionManager::receive_loop runs on a detached
+//     thread, SessionManager.cpp:703-854).
+//   * crypto::batch::* (Batch.hpp): many records per call, always on the MI355X; they throw
+//     std::invalid_argument / std::runtime_error (not reference signatures).
 //
 // Reference: src/crypto/{ChaCha20,Sha256,HmacSha256,CryptoManager}.cpp, src/security/StoreProof.cpp,
 // src/network/KeyManager.cpp and the PoW searches of src/core/Node.cpp (ShardianLabs/EphemeralNet).
@@ -16,15 +26,22 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <filesystem>
 #include <limits>
+#include <mutex>
+#include <new>
 #include <random>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "enet_crypto.h"
+#include "host_engine.hpp"
 
 namespace {
 
@@ -36,18 +53,82 @@ void enet_check(int rc, const char* what) {
     if (rc != ENET_OK) throw std::runtime_error(std::string("enet: ") + what + ": " + enet_last_error());
 }
 
-// Staging buffers + one stream per host thread: the reference functions are reentrant and
-// called from many session threads (SessionManager.cpp:332,703).  A scalar call is a GPU round
-// trip, so its fixed cost is what matters: buffers of up to kZeroCopyMax bytes
-// come from one pinned, device-mapped, coherent host blob -- "uploading" is a host memcpy into
-// it, the kernel reads its operands over PCIe and writes its results straight back, and
-// "downloading" is a memcpy after the stream sync -- so a small call costs one launch and one
-// sync instead of up to six pageable copies.  Larger buffers keep grow-only device slots and
-// async copies.  The blob is bump-allocated and rewound at every sync (every API call ends
-// with one), so no region is rewritten while a kernel of the same call may still read it.
+// ------------------------------------------------------------------------------ scalar routing
+namespace scalar {
+std::atomic<int> g_policy{ENET_SCALAR_AUTO};
+// ChaCha20 records from this size go to the MI355X under ENET_SCALAR_AUTO (INTEGRATION.md
+// measures the crossover: below it the host engine's AVX2 keystream beats PCIe + launch)
+std::atomic<uint64_t> g_crossover{256u << 10};
+std::atomic<int> g_on_error{0};
+std::atomic<uint64_t> g_host{0}, g_device{0}, g_failures{0}, g_launches{0}, g_records{0};
+std::atomic<uint32_t> g_inject{0};
+std::atomic<bool> g_reported{false};
+
+// does a call with a device kernel and `bytes` of payload go to the MI355X?
+bool device_for(uint64_t bytes, bool has_crossover) {
+    const int p = g_policy.load(std::memory_order_relaxed);
+    if (p == ENET_SCALAR_HOST) return false;
+    if (p == ENET_SCALAR_DEVICE) return true;
+    return has_crossover && bytes >= g_crossover.load(std::memory_order_relaxed);
+}
+
+void host_call() { g_host.fetch_add(1, std::memory_order_relaxed); }
+void device_call() { g_device.fetch_add(1, std::memory_order_relaxed); }
+
+// throws like a failed HIP call when a test injected failures
+void maybe_inject() {
+    uint32_t n = g_inject.load(std::memory_order_relaxed);
+    while (n > 0 && !g_inject.compare_exchange_weak(n, n - 1, std::memory_order_relaxed)) {
+    }
+    if (n > 0) throw std::runtime_error("enet: injected device failure (enet_scalar_inject_device_failures)");
+}
+
+// a device call of the scalar API failed: count it, say so once, finish on the host (or abort)
+void device_failed(const char* what, const char* why) noexcept {
+    g_failures.fetch_add(1, std::memory_order_relaxed);
+    if (g_on_error.load(std::memory_order_relaxed) == 1) {
+        std::fprintf(stderr, "enet: device path of %s failed (%s); aborting as configured\n", what, why);
+        std::abort();
+    }
+    if (!g_reported.exchange(true))
+        std::fprintf(stderr,
+                     "enet: device path of %s failed (%s); this and later failed scalar calls are "
+                     "finished on the host engine (enet_scalar_get_stats counts them)\n",
+                     what, why);
+}
+
+// Run `dev` (device path); on any failure except bad_alloc, report and return false.
+template <class F>
+bool try_device(const char* what, F&& dev) {
+    try {
+        maybe_inject();
+        dev();
+        device_call();
+        return true;
+    } catch (const std::bad_alloc&) {
+        throw;
+    } catch (const std::exception& e) {
+        device_failed(what, e.what());
+    } catch (...) {
+        device_failed(what, "unknown error");
+    }
+    return false;
+}
+}  // namespace scalar
+
+// Staging buffers + one stream per host thread, for the batch API and the scalar API's device
+// path under ENET_SCALAR_DEVICE.  Buffers of up to kZeroCopyMax bytes come from one pinned,
+// device-mapped, coherent host blob -- "uploading" is a host memcpy into it, the kernel reads
+// its operands over PCIe and writes its results straight back, and "downloading" is a memcpy
+// after the stream sync -- so a small call costs one launch and one sync instead of up to six
+// pageable copies.  The blob is 256 KiB (every small call fits: ~10 slots of <= 8 KiB; ADVICE r02:
+// 8 MiB per session thread pinned too much), allocated on the first small call of a thread.
+// Larger buffers keep grow-only device slots and async copies.  The blob is bump-allocated and
+// rewound at every sync (every API call ends with one), so no region is rewritten while a kernel
+// of the same call may still read it.
 struct Staging {
     static constexpr int kSlots = 10;
-    static constexpr size_t kHostBlob = 8u << 20;
+    static constexpr size_t kHostBlob = 256u << 10;
     static constexpr size_t kZeroCopyMax = 8u << 10;  // a serial SHA lane pays PCIe latency per block
     void* dev[kSlots] = {};
     size_t cap[kSlots] = {};
@@ -86,7 +167,11 @@ struct Staging {
             }
         }
         if (cap[slot] < bytes) {
-            if (dev[slot]) hip_check(hipFree(dev[slot]), "hipFree");
+            if (dev[slot]) {
+                (void)hipFree(dev[slot]);
+                dev[slot] = nullptr;
+                cap[slot] = 0;
+            }
             size_t c = std::max(bytes, cap[slot] * 2);
             hip_check(hipMalloc(&dev[slot], c), "hipMalloc");
             cap[slot] = c;
@@ -107,9 +192,18 @@ struct Staging {
         if (in_host(d)) pend.push_back({h, d, n});
         else hip_check(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, s()), "D2H");
     }
+    // Wait for the call's work, then run the deferred zero-copy downloads.  The pending list and
+    // the blob are released BEFORE the status check: a failed sync must not leave pointers into
+    // the caller's (about to be destroyed) vectors for the next call to write through.
     void sync() {
+        std::vector<Pending> todo;
+        todo.swap(pend);
+        used = 0;
         hip_check(hipStreamSynchronize(s()), "hipStreamSynchronize");
-        for (const Pending& q : pend) std::memcpy(q.dst, q.src, q.n);
+        for (const Pending& q : todo) std::memcpy(q.dst, q.src, q.n);
+    }
+    // drop queued downloads and rewind after a failed call
+    void reset() noexcept {
         pend.clear();
         used = 0;
     }
@@ -216,23 +310,226 @@ std::vector<uint8_t> flat_nonces(std::span<const ephemeralnet::crypto::Nonce> no
     return v;
 }
 
-std::array<uint8_t, 32> one_sha(std::span<const uint8_t> data) {
+// A throwing device call inside a Staging sequence: rewind the thread's staging before the
+// exception leaves, so the next call starts clean.
+template <class F>
+auto staged(F&& f) -> decltype(f(staging())) {
     Staging& st = staging();
-    std::span<const uint8_t> items[1] = {data};
-    Packed p = pack(items);
-    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
-    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
-    auto* dout = (uint8_t*)st.get(S_OUT, 32);
-    st.h2d(din, p.arena.data(), p.arena.size());
-    st.h2d(doff, p.off.data(), 16);
-    enet_check(enet_sha256_batch(1, din, doff, dout, st.s()), "sha256");
-    std::array<uint8_t, 32> d{};
-    st.d2h(d.data(), dout, 32);
-    st.sync();
-    return d;
+    st.reset();
+    try {
+        return f(st);
+    } catch (...) {
+        st.reset();
+        throw;
+    }
 }
 
+std::array<uint8_t, 32> device_sha(std::span<const uint8_t> data) {
+    return staged([&](Staging& st) {
+        std::span<const uint8_t> items[1] = {data};
+        Packed p = pack(items);
+        auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
+        auto* doff = (uint64_t*)st.get(S_INOFF, 16);
+        auto* dout = (uint8_t*)st.get(S_OUT, 32);
+        st.h2d(din, p.arena.data(), p.arena.size());
+        st.h2d(doff, p.off.data(), 16);
+        enet_check(enet_sha256_batch(1, din, doff, dout, st.s()), "sha256");
+        std::array<uint8_t, 32> d{};
+        st.d2h(d.data(), dout, 32);
+        st.sync();
+        return d;
+    });
+}
+
+std::array<uint8_t, 32> device_hmac(std::span<const uint8_t> key, std::span<const uint8_t> data) {
+    return staged([&](Staging& st) {
+        std::span<const uint8_t> items[1] = {data};
+        std::span<const uint8_t> kitems[1] = {key};
+        Packed p = pack(items);
+        Packed k = pack(kitems);
+        auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
+        auto* doff = (uint64_t*)st.get(S_INOFF, 16);
+        auto* dk = (uint8_t*)st.get(S_KEYS, k.arena.size());
+        auto* dkoff = (uint64_t*)st.get(S_OUTOFF, 16);
+        auto* dout = (uint8_t*)st.get(S_OUT, 32);
+        st.h2d(din, p.arena.data(), p.arena.size());
+        st.h2d(doff, p.off.data(), 16);
+        st.h2d(dk, k.arena.data(), k.arena.size());
+        st.h2d(dkoff, k.off.data(), 16);
+        enet_check(enet_hmac_sha256_batch(1, dk, dkoff, 0, din, doff, dout, st.s()), "hmac");
+        std::array<uint8_t, 32> m{};
+        st.d2h(m.data(), dout, 32);
+        st.sync();
+        return m;
+    });
+}
+
+// ------------------------------------------------------------------------------ coalescer
+// ChaCha20::apply records routed to the MI355X.  Each caller queues its request; whichever caller
+// finds no launch in flight becomes the leader, takes EVERY pending request, and runs them as one
+// enet_chacha20_xor_batch (one H2D per record straight from the caller's span, one launch, one
+// D2H per record straight into the caller's vector); requests arriving meanwhile wait for the
+// next leader.  No artificial delay: a lone caller launches at once, and under load the batch
+// grows by itself while the previous one runs.  The leader's staging is process-wide (one launch
+// in flight), so session threads do not each pin device buffers.
+struct ChachaReq {
+    const uint8_t* key;
+    const uint8_t* nonce;
+    uint32_t counter;
+    const uint8_t* in;
+    uint8_t* out;
+    size_t n;
+    bool done = false;
+    bool ok = false;
+};
+
+class Coalescer {
+public:
+    static Coalescer& get() {
+        static Coalescer* c = new Coalescer();  // never destroyed: no HIP calls during exit
+        return *c;
+    }
+    bool submit(ChachaReq& r) {
+        std::unique_lock<std::mutex> lk(mu_);
+        pending_.push_back(&r);
+        while (!r.done) {
+            if (busy_) {
+                cv_.wait(lk);
+                continue;
+            }
+            busy_ = true;
+            std::vector<ChachaReq*> batch;
+            batch.swap(pending_);
+            lk.unlock();
+            bool ok = false;
+            try {
+                scalar::maybe_inject();
+                run(batch);
+                ok = true;
+            } catch (const std::exception& e) {
+                st_.reset();
+                scalar::device_failed("ChaCha20::apply", e.what());
+            } catch (...) {
+                st_.reset();
+                scalar::device_failed("ChaCha20::apply", "unknown error");
+            }
+            lk.lock();
+            for (ChachaReq* q : batch) {
+                q->ok = ok;
+                q->done = true;
+            }
+            busy_ = false;
+            cv_.notify_all();
+        }
+        return r.ok;
+    }
+
+private:
+    void run(const std::vector<ChachaReq*>& batch) {
+        const size_t n = batch.size();
+        std::vector<uint64_t> off(n + 1, 0);
+        uint64_t mx = 0;
+        for (size_t i = 0; i < n; ++i) {
+            off[i + 1] = off[i] + batch[i]->n;
+            mx = std::max<uint64_t>(mx, batch[i]->n);
+        }
+        std::vector<uint8_t> meta(48 * n);  // keys [n][32], nonces [n][12], counters [n]
+        for (size_t i = 0; i < n; ++i) {
+            std::memcpy(meta.data() + 32 * i, batch[i]->key, 32);
+            std::memcpy(meta.data() + 32 * n + 12 * i, batch[i]->nonce, 12);
+            std::memcpy(meta.data() + 44 * n + 4 * i, &batch[i]->counter, 4);
+        }
+        auto* arena = (uint8_t*)st_.get(S_IN, off[n]);
+        auto* doff = (uint64_t*)st_.get(S_INOFF, 8 * (n + 1));
+        auto* dmeta = (uint8_t*)st_.get(S_KEYS, meta.size());
+        for (size_t i = 0; i < n; ++i) st_.h2d(arena + off[i], batch[i]->in, batch[i]->n);
+        st_.h2d(doff, off.data(), 8 * (n + 1));
+        st_.h2d(dmeta, meta.data(), meta.size());
+        enet_records r{};
+        r.count = (uint32_t)n;
+        r.in_offsets = doff;
+        r.out_offsets = doff;
+        r.in = arena;
+        r.out = arena;  // in place
+        r.keys = dmeta;
+        r.key_stride = 32;
+        r.nonces = dmeta + 32 * n;
+        r.total_bytes_hint = off[n];
+        r.max_len_hint = (uint32_t)std::min<uint64_t>(mx, 0xffffffffu);
+        enet_check(enet_chacha20_xor_batch(&r, reinterpret_cast<const uint32_t*>(dmeta + 44 * n), st_.s()),
+                   "chacha20 (coalesced)");
+        for (size_t i = 0; i < n; ++i) st_.d2h(batch[i]->out, arena + off[i], batch[i]->n);
+        st_.sync();
+        scalar::g_launches.fetch_add(1, std::memory_order_relaxed);
+        scalar::g_records.fetch_add(n, std::memory_order_relaxed);
+    }
+
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::vector<ChachaReq*> pending_;
+    bool busy_ = false;
+    Staging st_;
+};
+
 }  // namespace
+
+// ------------------------------------------------------------------------------ scalar C ABI
+extern "C" {
+
+int enet_scalar_set_policy(int policy, uint64_t crossover_bytes) {
+    if (policy != ENET_SCALAR_AUTO && policy != ENET_SCALAR_DEVICE && policy != ENET_SCALAR_HOST)
+        return ENET_EINVAL;
+    scalar::g_policy.store(policy, std::memory_order_relaxed);
+    if (crossover_bytes) scalar::g_crossover.store(crossover_bytes, std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+int enet_scalar_policy(void) { return scalar::g_policy.load(std::memory_order_relaxed); }
+
+int enet_scalar_set_on_device_error(int mode) {
+    if (mode != 0 && mode != 1) return ENET_EINVAL;
+    scalar::g_on_error.store(mode, std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+void enet_scalar_get_stats(enet_scalar_stats* out) {
+    if (!out) return;
+    out->host_calls = scalar::g_host.load();
+    out->device_calls = scalar::g_device.load();
+    out->device_failures = scalar::g_failures.load();
+    out->coalesced_launches = scalar::g_launches.load();
+    out->coalesced_records = scalar::g_records.load();
+}
+
+void enet_scalar_reset_stats(void) {
+    scalar::g_host = 0;
+    scalar::g_device = 0;
+    scalar::g_failures = 0;
+    scalar::g_launches = 0;
+    scalar::g_records = 0;
+}
+
+void enet_scalar_inject_device_failures(uint32_t n) { scalar::g_inject.store(n); }
+
+const char* enet_host_isa(void) { return enet::host::isa(); }
+
+void enet_host_chacha20_xor(const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                            const uint8_t* in, uint8_t* out, uint64_t n) {
+    enet::host::chacha20_xor(key, nonce, counter, in, out, n);
+}
+
+void enet_host_sha256(const uint8_t* in, uint64_t n, uint8_t digest[32]) {
+    const auto d = enet::host::sha256(in, n);
+    std::memcpy(digest, d.data(), 32);
+}
+
+void enet_host_hmac_sha256(const uint8_t* key, uint64_t key_len, const uint8_t* in, uint64_t n,
+                           uint8_t mac[32]) {
+    const auto m = enet::host::hmac_sha256(key, key_len, in, n);
+    std::memcpy(mac, m.data(), 32);
+}
+
+}  // extern "C"
 
 namespace ephemeralnet::crypto {
 
@@ -243,78 +540,108 @@ void ChaCha20::apply(const Key& key, const Nonce& nonce, std::span<const std::ui
         output.clear();
         return;
     }
-    std::span<const uint8_t> items[1] = {input};
-    const std::span<const Key> ks(&key, 1);
-    const std::span<const Nonce> ns(&nonce, 1);
-    const std::uint32_t ctr[1] = {counter};
-    auto res = batch::chacha20_apply(ks, ns, items, ctr);
-    output = std::move(res[0]);
+    const size_t n = input.size();
+    // the input may alias the output vector (in-place use): copy it before resizing moves it
+    std::vector<uint8_t> keep;
+    const uint8_t* in = input.data();
+    if (!output.empty() && in >= output.data() && in < output.data() + output.size() && n > output.size()) {
+        keep.assign(input.begin(), input.end());
+        in = keep.data();
+    }
+    output.resize(n);
+    if (scalar::device_for(n, true)) {
+        ChachaReq r{key.bytes.data(), nonce.bytes.data(), counter, in, output.data(), n};
+        bool ok = false;
+        try {
+            ok = Coalescer::get().submit(r);
+        } catch (const std::bad_alloc&) {
+            throw;
+        } catch (...) {
+            scalar::device_failed("ChaCha20::apply", "coalescer error");
+        }
+        if (ok) {
+            scalar::device_call();
+            return;
+        }
+    }
+    scalar::host_call();
+    enet::host::chacha20_xor(key.bytes.data(), nonce.bytes.data(), counter, in, output.data(), n);
 }
 
 // ------------------------------------------------------------------------------ SHA-256
-Sha256::Sha256() = default;
-
-void Sha256::update(std::span<const std::uint8_t> data) {
-    pending_.insert(pending_.end(), data.begin(), data.end());
+// Streaming over the reference's own member layout (Sha256.hpp): 64-byte buffer, running state.
+Sha256::Sha256() {
+    std::memcpy(state_.data(), enet::host::kIV, sizeof(enet::host::kIV));
 }
 
-std::array<std::uint8_t, 32> Sha256::finalize() {
-    auto d = one_sha(pending_);
-    std::fill(pending_.begin(), pending_.end(), 0);  // finalize resets (Sha256.cpp:122-124)
-    pending_.clear();
+void Sha256::transform(const std::uint8_t block[64]) { enet::host::sha256_blocks(state_.data(), block, 1); }
+
+void Sha256::update(std::span<const std::uint8_t> data) {  // Sha256.cpp:72-92
+    const uint8_t* p = data.data();
+    size_t n = data.size();
+    if (!n) return;
+    bit_len_ += (std::uint64_t)n * 8u;
+    if (buffer_size_) {
+        const size_t m = std::min(n, 64 - buffer_size_);
+        std::memcpy(buffer_.data() + buffer_size_, p, m);
+        buffer_size_ += m;
+        p += m;
+        n -= m;
+        if (buffer_size_ < 64) return;
+        transform(buffer_.data());
+        buffer_size_ = 0;
+    }
+    const size_t whole = n / 64;
+    enet::host::sha256_blocks(state_.data(), p, whole);
+    p += 64 * whole;
+    n -= 64 * whole;
+    if (n) std::memcpy(buffer_.data(), p, n);
+    buffer_size_ = n;
+}
+
+std::array<std::uint8_t, 32> Sha256::finalize() {  // Sha256.cpp:94-126 (resets the hasher)
+    enet::host::Sha256State s;
+    std::memcpy(s.h, state_.data(), 32);
+    std::memcpy(s.buf, buffer_.data(), 64);
+    s.fill = buffer_size_;
+    s.bits = bit_len_;
+    const auto d = enet::host::sha256_final(s);
+    std::memcpy(state_.data(), enet::host::kIV, sizeof(enet::host::kIV));
+    buffer_.fill(0);
+    buffer_size_ = 0;
+    bit_len_ = 0;
+    scalar::host_call();
     return d;
 }
 
-std::array<std::uint8_t, 32> Sha256::digest(std::span<const std::uint8_t> data) { return one_sha(data); }
+std::array<std::uint8_t, 32> Sha256::digest(std::span<const std::uint8_t> data) {
+    // one message = one serial chain: the host engine unless the caller forced the device
+    if (scalar::device_for(data.size(), false)) {
+        std::array<std::uint8_t, 32> d{};
+        if (scalar::try_device("Sha256::digest", [&] { d = device_sha(data); })) return d;
+    }
+    scalar::host_call();
+    return enet::host::sha256(data.data(), data.size());
+}
 
 // ------------------------------------------------------------------------------ HMAC
 std::array<std::uint8_t, HmacSha256::kDigestSize> HmacSha256::compute(std::span<const std::uint8_t> key,
                                                                       std::span<const std::uint8_t> data) {
-    Staging& st = staging();
-    std::span<const uint8_t> items[1] = {data};
-    std::span<const uint8_t> kitems[1] = {key};
-    Packed p = pack(items);
-    Packed k = pack(kitems);
-    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
-    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
-    auto* dk = (uint8_t*)st.get(S_KEYS, k.arena.size());
-    auto* dkoff = (uint64_t*)st.get(S_OUTOFF, 16);
-    auto* dout = (uint8_t*)st.get(S_OUT, 32);
-    st.h2d(din, p.arena.data(), p.arena.size());
-    st.h2d(doff, p.off.data(), 16);
-    st.h2d(dk, k.arena.data(), k.arena.size());
-    st.h2d(dkoff, k.off.data(), 16);
-    enet_check(enet_hmac_sha256_batch(1, dk, dkoff, 0, din, doff, dout, st.s()), "hmac");
-    std::array<uint8_t, 32> m{};
-    st.d2h(m.data(), dout, 32);
-    st.sync();
-    return m;
+    if (scalar::device_for(data.size(), false)) {
+        std::array<std::uint8_t, 32> m{};
+        if (scalar::try_device("HmacSha256::compute", [&] { m = device_hmac(key, data); })) return m;
+    }
+    scalar::host_call();
+    return enet::host::hmac_sha256(key.data(), key.size(), data.data(), data.size());
 }
 
 bool HmacSha256::verify(std::span<const std::uint8_t> key, std::span<const std::uint8_t> data,
                         std::span<const std::uint8_t> mac) {
     if (mac.size() != kDigestSize) return false;  // HmacSha256.cpp:44
-    Staging& st = staging();
-    std::span<const uint8_t> items[1] = {data};
-    std::span<const uint8_t> kitems[1] = {key};
-    Packed p = pack(items);
-    Packed k = pack(kitems);
-    auto* din = (uint8_t*)st.get(S_IN, p.arena.size());
-    auto* doff = (uint64_t*)st.get(S_INOFF, 16);
-    auto* dk = (uint8_t*)st.get(S_KEYS, k.arena.size());
-    auto* dkoff = (uint64_t*)st.get(S_OUTOFF, 16);
-    auto* dmac = (uint8_t*)st.get(S_TAGS, 32);
-    auto* dok = (uint8_t*)st.get(S_OK, 4);
-    st.h2d(din, p.arena.data(), p.arena.size());
-    st.h2d(doff, p.off.data(), 16);
-    st.h2d(dk, k.arena.data(), k.arena.size());
-    st.h2d(dkoff, k.off.data(), 16);
-    st.h2d(dmac, mac.data(), 32);
-    enet_check(enet_hmac_sha256_verify_batch(1, dk, dkoff, 0, din, doff, dmac, dok, st.s()), "hmac verify");
-    uint8_t ok = 0;
-    st.d2h(&ok, dok, 1);
-    st.sync();
-    return ok == 1;
+    const auto expect = compute(key, data);
+    std::uint8_t diff = 0;  // OR-accumulate, no early exit (HmacSha256.cpp:48-53)
+    for (size_t i = 0; i < kDigestSize; ++i) diff |= static_cast<std::uint8_t>(expect[i] ^ mac[i]);
+    return diff == 0;
 }
 
 // ------------------------------------------------------------------------------ CryptoManager
@@ -385,6 +712,7 @@ std::vector<std::vector<std::uint8_t>> chacha20_apply(std::span<const Key> keys,
         throw std::invalid_argument("enet batch::chacha20_apply: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(inputs);
     auto kf = flat_keys(keys);
     auto nf = flat_nonces(nonces);
@@ -405,6 +733,7 @@ std::vector<Sealed> aead_seal(std::span<const Key> keys, std::span<const Nonce> 
     if (keys.size() != n || nonces.size() != n) throw std::invalid_argument("enet batch::aead_seal: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(plaintexts);
     auto kf = flat_keys(keys);
     auto nf = flat_nonces(nonces);
@@ -432,6 +761,7 @@ std::vector<std::vector<std::uint8_t>> aead_open(std::span<const Key> keys, std:
     ok.assign(n, 0);
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(ciphertexts);
     auto kf = flat_keys(keys);
     auto nf = flat_nonces(nonces);
@@ -448,6 +778,7 @@ std::vector<std::array<std::uint8_t, 32>> sha256(std::span<const std::span<const
     const size_t n = messages.size();
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(messages);
     auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
     auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
@@ -469,6 +800,7 @@ std::vector<std::vector<std::uint8_t>> frame_seal(std::span<const std::array<std
         throw std::invalid_argument("enet batch::frame_seal: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(messages);
     auto out_off = offsets_of(messages, 32);
     auto nf = flat_nonces(nonces);
@@ -487,6 +819,7 @@ std::vector<std::vector<std::uint8_t>> frame_open(std::span<const std::array<std
     ok.assign(n, 0);
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(bodies);
     auto out_off = offsets_of(bodies, -32);
     auto nf = flat_nonces(nonces);
@@ -506,6 +839,7 @@ std::vector<StoredChunk> chunk_store(std::span<const Key> keys, std::span<const 
         throw std::invalid_argument("enet batch::chunk_store: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(chunks);
     auto kf = flat_keys(keys);
     auto nf = flat_nonces(nonces);
@@ -539,6 +873,7 @@ std::vector<std::vector<std::uint8_t>> chunk_fetch(std::span<const Key> keys, st
     ok.assign(n, 0);
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(ciphertexts);
     auto kf = flat_keys(keys);
     auto nf = flat_nonces(nonces);
@@ -561,6 +896,7 @@ std::vector<std::vector<std::uint8_t>> wire_seal(std::span<const std::array<std:
         throw std::invalid_argument("enet batch::wire_seal: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(messages);
     auto out_off = offsets_of(messages, 16 + 32);
     auto nf = flat_nonces(nonces);
@@ -577,6 +913,7 @@ std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std:
     ok.assign(n, 0);
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(frames);
     auto out_off = offsets_of(frames, -(16 + 32));
     std::vector<uint8_t> no_nonces(12 * n, 0);  // unused: the nonce travels in the frame
@@ -626,6 +963,7 @@ std::vector<PowResult> pow_search(std::span<const std::span<const std::uint8_t>>
     if (difficulty.size() != n) throw std::invalid_argument("enet batch::pow_search: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(prefixes);
     auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
     auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
@@ -658,6 +996,7 @@ std::vector<std::uint8_t> pow_check(std::span<const std::span<const std::uint8_t
         throw std::invalid_argument("enet batch::pow_check: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     Packed in = pack(prefixes);
     auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
     auto* doff = (uint64_t*)st.get(S_INOFF, 8 * (n + 1));
@@ -701,17 +1040,47 @@ std::vector<std::uint8_t> handshake_pow_prefix(const PeerId& initiator, const Pe
 }
 
 namespace {
+// Node.cpp:212-230 / 269-292 on the host engine: start = first mt19937_64 draw seeded by the
+// big-endian first 8 digest bytes of nonce 0, candidates start + attempt
+bool host_node_pow(const std::vector<std::uint8_t>& prefix, std::uint8_t difficulty, std::uint64_t max_attempts,
+                   std::uint64_t& nonce_out) {
+    enet::host::PowPrefix pp;
+    enet::host::pow_prefix(pp, prefix.data(), prefix.size());
+    const auto d0 = enet::host::pow_digest(pp, 0);
+    std::uint64_t seed = 0;
+    for (int i = 0; i < 8; ++i) seed = (seed << 8) | d0[i];
+    std::mt19937_64 gen(seed);
+    std::uniform_int_distribution<std::uint64_t> dist(0, std::numeric_limits<std::uint64_t>::max());
+    const std::uint64_t start = dist(gen);
+    for (std::uint64_t a = 0; a < max_attempts; ++a) {
+        if (enet::host::leading_zero_bits(enet::host::pow_digest(pp, start + a)) >= difficulty) {
+            nonce_out = start + a;
+            return true;
+        }
+    }
+    return false;
+}
+
 bool node_pow_one(const std::vector<std::uint8_t>& prefix, std::uint8_t difficulty, std::uint64_t& nonce_out) {
     if (difficulty == 0) {  // Node.cpp:213-216 / 274-277
         nonce_out = 0;
         return true;
     }
-    const std::span<const std::uint8_t> ps[1] = {prefix};
-    const std::uint8_t d[1] = {difficulty};
-    const auto r = pow_search(ps, d, PowSchedule::Node, kNodePowAttempts);
-    if (!r[0].found) return false;
-    nonce_out = r[0].nonce;
-    return true;
+    // a search: the MI355X unless the caller chose the host (never throws: a reference drop-in)
+    if (scalar::device_for(0, false) || scalar::g_policy.load() == ENET_SCALAR_AUTO) {
+        PowResult r{};
+        if (scalar::try_device("compute_*_pow", [&] {
+                const std::span<const std::uint8_t> ps[1] = {prefix};
+                const std::uint8_t d[1] = {difficulty};
+                r = pow_search(ps, d, PowSchedule::Node, kNodePowAttempts)[0];
+            })) {
+            if (!r.found) return false;
+            nonce_out = r.nonce;
+            return true;
+        }
+    }
+    scalar::host_call();
+    return host_node_pow(prefix, difficulty, kNodePowAttempts, nonce_out);
 }
 }  // namespace
 
@@ -735,6 +1104,7 @@ std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secr
         throw std::invalid_argument("enet batch::session_keys: size mismatch");
     if (n == 0) return {};
     Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
     auto kf = flat_keys(secrets);
     auto* dk = (uint8_t*)st.get(S_KEYS, 32 * n);
     auto* dc = (uint64_t*)st.get(S_CTR, 8 * n);
@@ -756,7 +1126,9 @@ std::vector<std::array<std::uint8_t, 32>> session_keys(std::span<const Key> secr
 // ------------------------------------------------------------------------------ security::StoreProof
 namespace ephemeralnet::security {
 
-ChunkId derive_chunk_id(std::span<const std::uint8_t> data) { return one_sha(data); }
+ChunkId derive_chunk_id(std::span<const std::uint8_t> data) {  // StoreProof.cpp:75-78
+    return crypto::Sha256::digest(data);
+}
 
 std::optional<std::string> sanitize_filename_hint(std::string_view raw_path) {
     if (raw_path.empty()) return std::nullopt;
@@ -821,13 +1193,61 @@ std::vector<std::uint8_t> store_pow_valid(std::span<const StoreWorkInput> inputs
 }
 }  // namespace batch
 
+namespace {
+// StoreProof.cpp:47-69 on the host engine
+bool host_store_pow_valid(const StoreWorkInput& input, std::uint64_t nonce, std::uint8_t d) {
+    const auto pre = store_pow_prefix(input);
+    enet::host::PowPrefix pp;
+    enet::host::pow_prefix(pp, pre.data(), pre.size());
+    return enet::host::leading_zero_bits(enet::host::pow_digest(pp, nonce)) >= d;
+}
+
+// StoreProof.cpp:123-146 on the host engine: successive mt19937_64 outputs seeded by the
+// native-endian (x86: little-endian) first 8 digest bytes of nonce 0
+std::optional<std::uint64_t> host_store_pow(const StoreWorkInput& input, std::uint8_t d, std::uint64_t max_attempts) {
+    const auto pre = store_pow_prefix(input);
+    enet::host::PowPrefix pp;
+    enet::host::pow_prefix(pp, pre.data(), pre.size());
+    const auto d0 = enet::host::pow_digest(pp, 0);
+    std::uint64_t seed = 0;
+    std::memcpy(&seed, d0.data(), sizeof(seed));
+    std::mt19937_64 rng(seed);
+    for (std::uint64_t a = 0; a < max_attempts; ++a) {
+        const std::uint64_t c = rng();
+        if (enet::host::leading_zero_bits(enet::host::pow_digest(pp, c)) >= d) return c;
+    }
+    return std::nullopt;
+}
+}  // namespace
+
 bool store_pow_valid(const StoreWorkInput& input, std::uint64_t nonce, std::uint8_t difficulty_bits) {
-    return batch::store_pow_valid(std::span(&input, 1), std::span(&nonce, 1), difficulty_bits)[0] == 1;
+    if (difficulty_bits == 0) return true;  // StoreProof.cpp:112-113
+    const std::uint8_t d = clamp_store_difficulty(difficulty_bits);
+    if (scalar::device_for(0, false)) {  // one hash: the host engine unless forced
+        std::uint8_t ok = 0;
+        if (scalar::try_device("store_pow_valid", [&] {
+                ok = batch::store_pow_valid(std::span(&input, 1), std::span(&nonce, 1), difficulty_bits)[0];
+            }))
+            return ok == 1;
+    }
+    scalar::host_call();
+    return host_store_pow_valid(input, nonce, d);
 }
 
 std::optional<std::uint64_t> compute_store_pow(const StoreWorkInput& input, std::uint8_t difficulty_bits,
                                                std::uint64_t max_attempts) {
-    return batch::compute_store_pow(std::span(&input, 1), difficulty_bits, max_attempts)[0];
+    if (difficulty_bits == 0) return std::uint64_t{0};  // StoreProof.cpp:125-127
+    const std::uint8_t d = clamp_store_difficulty(difficulty_bits);
+    if (max_attempts == 0) max_attempts = kDefaultStorePowMaxAttempts;  // :131-133
+    if (scalar::g_policy.load() != ENET_SCALAR_HOST) {  // a search: the MI355X
+        std::optional<std::uint64_t> r;
+        if (scalar::try_device("compute_store_pow", [&] {
+                r = batch::compute_store_pow(std::span(&input, 1), difficulty_bits, max_attempts)[0];
+            }))
+            return r;
+    }
+    scalar::host_call();
+    return host_store_pow(input, d, max_attempts);
 }
 
 }  // namespace ephemeralnet::security
@@ -876,9 +1296,15 @@ std::optional<std::array<std::uint8_t, 32>> KeyManager::rotate_if_needed(
     if (now - context.last_rotation < rotation_interval_) return std::nullopt;  // :63-65
     context.counter += 1;
     context.last_rotation = now;
-    const std::uint64_t ctr[1] = {context.counter};
-    const std::int64_t tk[1] = {ticks_of(now)};
-    context.current_key = crypto::batch::session_keys(std::span(&context.shared_secret, 1), ctr, tk)[0];
+    // derive_key (KeyManager.cpp:74-92): HMAC(secret, BE64(counter) || BE64(ticks)) -- one HMAC,
+    // so the host engine unless the caller forced the device (HmacSha256::compute routes it)
+    std::array<std::uint8_t, 16> material{};
+    const std::uint64_t ticks = static_cast<std::uint64_t>(ticks_of(now));
+    for (int i = 0; i < 8; ++i) {
+        material[i] = static_cast<std::uint8_t>(context.counter >> (56 - 8 * i));
+        material[8 + i] = static_cast<std::uint8_t>(ticks >> (56 - 8 * i));
+    }
+    context.current_key = crypto::HmacSha256::compute(context.shared_secret.bytes, material);
     return context.current_key;
 }
 
@@ -909,7 +1335,22 @@ std::vector<std::pair<PeerId, std::array<std::uint8_t, 32>>> KeyManager::rotate_
     }
     std::vector<std::pair<PeerId, std::array<std::uint8_t, 32>>> out;
     if (due.empty()) return out;
-    auto keys = crypto::batch::session_keys(secrets, counters, ticks);
+    // many sessions: one device batch; a failed device call is finished on the host engine
+    std::vector<std::array<std::uint8_t, 32>> keys;
+    if (!(scalar::g_policy.load() != ENET_SCALAR_HOST &&
+          scalar::try_device("KeyManager::rotate_all_due",
+                             [&] { keys = crypto::batch::session_keys(secrets, counters, ticks); }))) {
+        scalar::host_call();
+        keys.resize(due.size());
+        for (size_t i = 0; i < due.size(); ++i) {
+            std::array<std::uint8_t, 16> m{};
+            for (int b = 0; b < 8; ++b) {
+                m[b] = static_cast<std::uint8_t>(counters[i] >> (56 - 8 * b));
+                m[8 + b] = static_cast<std::uint8_t>(static_cast<std::uint64_t>(ticks[i]) >> (56 - 8 * b));
+            }
+            keys[i] = enet::host::hmac_sha256(secrets[i].bytes.data(), 32, m.data(), m.size());
+        }
+    }
     out.reserve(due.size());
     for (size_t i = 0; i < due.size(); ++i) {
         due[i]->counter = counters[i];

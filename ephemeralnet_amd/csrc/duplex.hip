@@ -84,14 +84,18 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
 
     // ---- geometry (both lanes of a record compute it)
     uint64_t ib = 0, Li = 0, ob = 0, Lo = 0;
+    bool ordered = true;  // offsets non-decreasing: a decreasing pair would wrap Li / Lo to ~2^64
     if (live) {
         ib = p.in_off[rec];
-        Li = p.in_off[rec + 1] - ib;
+        const uint64_t ie = p.in_off[rec + 1];
         ob = p.out_off[rec];
-        Lo = p.out_off[rec + 1] - ob;
+        const uint64_t oe = p.out_off[rec + 1];
+        ordered = ie >= ib && oe >= ob;
+        Li = ordered ? ie - ib : 0u;
+        Lo = ordered ? oe - ob : 0u;  // nothing is zeroed for a disordered record
     }
     uint64_t Lm = 0;  // message bytes
-    bool valid = live;
+    bool valid = live && ordered;
     if (KIND == DK_FRAME && !OPEN) {
         Lm = Li;
         valid = valid && Lo == Li + 32u + H;

@@ -1,0 +1,400 @@
+// host_engine.cpp -- scalar SHA-256 / HMAC-SHA256 / ChaCha20 on the calling CPU thread
+// (host_engine.hpp says why).  x86-64: SHA-256 on the SHA extensions (sha256rnds2 / msg1 /
+// msg2), ChaCha20 eight blocks at a time in AVX2 registers (one 32-bit state word of eight
+// blocks per ymm register, counters base + 0..7 wrapping mod 2^32 like ChaCha20.cpp:110), both
+// picked at run time from cpuid; portable C++ otherwise and for the tails.
+#include "host_engine.hpp"
+
+#include <atomic>
+#include <cstring>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+namespace enet::host {
+
+namespace {
+
+constexpr std::uint32_t kK[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u,
+    0xab1c5ed5u, 0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu,
+    0x9bdc06a7u, 0xc19bf174u, 0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu,
+    0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau, 0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u,
+    0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u, 0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu,
+    0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u, 0xa2bfe8a1u, 0xa81a664bu,
+    0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u, 0x19a4c116u,
+    0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u,
+    0xc67178f2u};
+
+inline std::uint32_t rotr(std::uint32_t v, int s) { return (v >> s) | (v << (32 - s)); }
+inline std::uint32_t rotl(std::uint32_t v, int s) { return (v << s) | (v >> (32 - s)); }
+inline std::uint32_t be32(const std::uint8_t* p) {
+    return (std::uint32_t)p[0] << 24 | (std::uint32_t)p[1] << 16 | (std::uint32_t)p[2] << 8 | p[3];
+}
+inline std::uint32_t le32(const std::uint8_t* p) {
+    std::uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;  // x86-64 / aarch64 hosts are little-endian
+}
+
+std::atomic<bool> g_portable{false};
+
+// ------------------------------------------------------------------------------ SHA-256
+void sha256_portable(std::uint32_t st[8], const std::uint8_t* p, std::size_t blocks) {
+    for (; blocks; --blocks, p += 64) {
+        std::uint32_t w[16];
+        for (int i = 0; i < 16; ++i) w[i] = be32(p + 4 * i);
+        std::uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
+                      h = st[7];
+        for (int i = 0; i < 64; ++i) {
+            if (i >= 16) {
+                const std::uint32_t x = w[(i - 15) & 15], y = w[(i - 2) & 15];
+                w[i & 15] += (rotr(y, 17) ^ rotr(y, 19) ^ (y >> 10)) + w[(i - 7) & 15] +
+                             (rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3));
+            }
+            const std::uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) +
+                                     ((e & f) ^ (~e & g)) + kK[i] + w[i & 15];
+            const std::uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+        st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+}
+
+#if defined(__x86_64__)
+// SHA extensions: the state lives as ABEF / CDGH pairs, sha256rnds2 does two rounds with the
+// message+constant words in the low half of its third operand; msg1 / msg2 extend the schedule.
+// Schedule vector g holds words 4g..4g+3:
+//   W(g) = msg2(msg1(W(g-4), W(g-3)) + alignr(W(g-1), W(g-2), 4), W(g-1)).
+__attribute__((target("sha,sse4.1,ssse3"))) void sha256_shani(std::uint32_t st[8], const std::uint8_t* p,
+                                                             std::size_t blocks) {
+    const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bll, 0x0405060700010203ll);
+    __m128i t = _mm_loadu_si128(reinterpret_cast<const __m128i*>(st));       // a b c d
+    __m128i s1 = _mm_loadu_si128(reinterpret_cast<const __m128i*>(st + 4));  // e f g h
+    t = _mm_shuffle_epi32(t, 0xB1);                                           // b a d c
+    s1 = _mm_shuffle_epi32(s1, 0x1B);                                         // h g f e
+    __m128i s0 = _mm_alignr_epi8(t, s1, 8);                                   // ABEF
+    s1 = _mm_blend_epi16(s1, t, 0xF0);                                        // CDGH
+    for (; blocks; --blocks, p += 64) {
+        const __m128i save0 = s0, save1 = s1;
+        __m128i w[4];
+        for (int g = 0; g < 16; ++g) {
+            if (g < 4) {
+                w[g] = _mm_shuffle_epi8(_mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * g)), bswap);
+            } else {
+                const __m128i m = _mm_add_epi32(_mm_sha256msg1_epu32(w[g & 3], w[(g - 3) & 3]),
+                                                _mm_alignr_epi8(w[(g - 1) & 3], w[(g - 2) & 3], 4));
+                w[g & 3] = _mm_sha256msg2_epu32(m, w[(g - 1) & 3]);
+            }
+            __m128i k = _mm_add_epi32(w[g & 3], _mm_loadu_si128(reinterpret_cast<const __m128i*>(kK + 4 * g)));
+            s1 = _mm_sha256rnds2_epu32(s1, s0, k);
+            k = _mm_shuffle_epi32(k, 0x0E);
+            s0 = _mm_sha256rnds2_epu32(s0, s1, k);
+        }
+        s0 = _mm_add_epi32(s0, save0);
+        s1 = _mm_add_epi32(s1, save1);
+    }
+    t = _mm_shuffle_epi32(s0, 0x1B);   // F E B A
+    s1 = _mm_shuffle_epi32(s1, 0xB1);  // D C H G
+    s0 = _mm_blend_epi16(t, s1, 0xF0); // D C B A
+    s1 = _mm_alignr_epi8(s1, t, 8);    // H G F E
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st), s0);
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(st + 4), s1);
+}
+#endif
+
+bool have_shani() {
+#if defined(__x86_64__)
+    static const bool v = __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+    return v;
+#else
+    return false;
+#endif
+}
+
+bool have_avx2() {
+#if defined(__x86_64__)
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+#else
+    return false;
+#endif
+}
+
+// ------------------------------------------------------------------------------ ChaCha20
+constexpr std::uint32_t kSigma[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+
+#define ENET_HQR(a, b, c, d)                \
+    a += b; d ^= a; d = rotl(d, 16);        \
+    c += d; b ^= c; b = rotl(b, 12);        \
+    a += b; d ^= a; d = rotl(d, 8);         \
+    c += d; b ^= c; b = rotl(b, 7)
+
+void chacha_block(const std::uint32_t in[16], std::uint32_t out[16]) {
+    std::uint32_t x[16];
+    std::memcpy(x, in, sizeof(x));
+    for (int r = 0; r < 10; ++r) {
+        ENET_HQR(x[0], x[4], x[8], x[12]);
+        ENET_HQR(x[1], x[5], x[9], x[13]);
+        ENET_HQR(x[2], x[6], x[10], x[14]);
+        ENET_HQR(x[3], x[7], x[11], x[15]);
+        ENET_HQR(x[0], x[5], x[10], x[15]);
+        ENET_HQR(x[1], x[6], x[11], x[12]);
+        ENET_HQR(x[2], x[7], x[8], x[13]);
+        ENET_HQR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+// one block at a time: x ^= keystream(state), state[12]++ (u32 wrap)
+void chacha_portable(std::uint32_t s[16], const std::uint8_t* in, std::uint8_t* out, std::size_t n) {
+    std::uint32_t ks[16];
+    std::uint8_t kb[64];
+    while (n) {
+        chacha_block(s, ks);
+        s[12] += 1u;
+        for (int i = 0; i < 16; ++i) std::memcpy(kb + 4 * i, &ks[i], 4);
+        const std::size_t m = n < 64 ? n : 64;
+        for (std::size_t i = 0; i < m; ++i) out[i] = in[i] ^ kb[i];
+        in += m;
+        out += m;
+        n -= m;
+    }
+    volatile std::uint8_t* vk = kb;  // wipe the keystream (ChaCha20.cpp:120)
+    for (int i = 0; i < 64; ++i) vk[i] = 0;
+    std::memset(ks, 0, sizeof(ks));
+}
+
+#if defined(__x86_64__)
+// Eight blocks per step, counters s[12] + 0..7; n8 = whole 512-byte steps.
+__attribute__((target("avx2"))) void chacha_avx2(std::uint32_t s[16], const std::uint8_t* in,
+                                                std::uint8_t* out, std::size_t n8) {
+    const __m256i r16 = _mm256_set_epi8(13, 12, 15, 14, 9, 8, 11, 10, 5, 4, 7, 6, 1, 0, 3, 2,
+                                        13, 12, 15, 14, 9, 8, 11, 10, 5, 4, 7, 6, 1, 0, 3, 2);
+    const __m256i r8 = _mm256_set_epi8(14, 13, 12, 15, 10, 9, 8, 11, 6, 5, 4, 7, 2, 1, 0, 3,
+                                       14, 13, 12, 15, 10, 9, 8, 11, 6, 5, 4, 7, 2, 1, 0, 3);
+    const __m256i lanes = _mm256_set_epi32(7, 6, 5, 4, 3, 2, 1, 0);
+    __m256i init[16];
+    for (int i = 0; i < 16; ++i) init[i] = _mm256_set1_epi32((int)s[i]);
+#define ENET_VROT(v, r) _mm256_or_si256(_mm256_slli_epi32(v, r), _mm256_srli_epi32(v, 32 - r))
+#define ENET_VQR(a, b, c, d)                                                            \
+    a = _mm256_add_epi32(a, b); d = _mm256_shuffle_epi8(_mm256_xor_si256(d, a), r16);  \
+    c = _mm256_add_epi32(c, d); b = _mm256_xor_si256(b, c); b = ENET_VROT(b, 12);      \
+    a = _mm256_add_epi32(a, b); d = _mm256_shuffle_epi8(_mm256_xor_si256(d, a), r8);   \
+    c = _mm256_add_epi32(c, d); b = _mm256_xor_si256(b, c); b = ENET_VROT(b, 7)
+    for (; n8; --n8, in += 512, out += 512) {
+        init[12] = _mm256_add_epi32(_mm256_set1_epi32((int)s[12]), lanes);  // u32 wrap per lane
+        __m256i x[16];
+        for (int i = 0; i < 16; ++i) x[i] = init[i];
+        for (int r = 0; r < 10; ++r) {
+            ENET_VQR(x[0], x[4], x[8], x[12]);
+            ENET_VQR(x[1], x[5], x[9], x[13]);
+            ENET_VQR(x[2], x[6], x[10], x[14]);
+            ENET_VQR(x[3], x[7], x[11], x[15]);
+            ENET_VQR(x[0], x[5], x[10], x[15]);
+            ENET_VQR(x[1], x[6], x[11], x[12]);
+            ENET_VQR(x[2], x[7], x[8], x[13]);
+            ENET_VQR(x[3], x[4], x[9], x[14]);
+        }
+        for (int i = 0; i < 16; ++i) x[i] = _mm256_add_epi32(x[i], init[i]);
+        // transpose each 8x8 (word x block) half into per-block rows: half 0 = words 0..7
+        // (bytes 0..31 of every block), half 1 = words 8..15 (bytes 32..63)
+        for (int half = 0; half < 2; ++half) {
+            const __m256i* a = x + 8 * half;
+            const __m256i t0 = _mm256_unpacklo_epi32(a[0], a[1]), t1 = _mm256_unpackhi_epi32(a[0], a[1]);
+            const __m256i t2 = _mm256_unpacklo_epi32(a[2], a[3]), t3 = _mm256_unpackhi_epi32(a[2], a[3]);
+            const __m256i t4 = _mm256_unpacklo_epi32(a[4], a[5]), t5 = _mm256_unpackhi_epi32(a[4], a[5]);
+            const __m256i t6 = _mm256_unpacklo_epi32(a[6], a[7]), t7 = _mm256_unpackhi_epi32(a[6], a[7]);
+            const __m256i u0 = _mm256_unpacklo_epi64(t0, t2), u1 = _mm256_unpackhi_epi64(t0, t2);
+            const __m256i u2 = _mm256_unpacklo_epi64(t1, t3), u3 = _mm256_unpackhi_epi64(t1, t3);
+            const __m256i u4 = _mm256_unpacklo_epi64(t4, t6), u5 = _mm256_unpackhi_epi64(t4, t6);
+            const __m256i u6 = _mm256_unpacklo_epi64(t5, t7), u7 = _mm256_unpackhi_epi64(t5, t7);
+            const __m256i rows[8] = {
+                _mm256_permute2x128_si256(u0, u4, 0x20), _mm256_permute2x128_si256(u1, u5, 0x20),
+                _mm256_permute2x128_si256(u2, u6, 0x20), _mm256_permute2x128_si256(u3, u7, 0x20),
+                _mm256_permute2x128_si256(u0, u4, 0x31), _mm256_permute2x128_si256(u1, u5, 0x31),
+                _mm256_permute2x128_si256(u2, u6, 0x31), _mm256_permute2x128_si256(u3, u7, 0x31)};
+            for (int b = 0; b < 8; ++b) {
+                const std::size_t o = 64 * (std::size_t)b + 32 * (std::size_t)half;
+                const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(in + o));
+                _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + o), _mm256_xor_si256(v, rows[b]));
+            }
+        }
+        s[12] += 8u;
+    }
+#undef ENET_VQR
+#undef ENET_VROT
+    _mm256_zeroupper();
+}
+#endif
+
+}  // namespace
+
+void force_portable(bool on) { g_portable.store(on, std::memory_order_relaxed); }
+
+const char* isa() {
+    if (g_portable.load(std::memory_order_relaxed)) return "portable";
+    const bool s = have_shani(), a = have_avx2();
+    return s && a ? "sha-ni+avx2" : s ? "sha-ni" : a ? "avx2" : "portable";
+}
+
+void sha256_blocks(std::uint32_t state[8], const std::uint8_t* p, std::size_t blocks) {
+    if (!blocks) return;
+#if defined(__x86_64__)
+    if (have_shani() && !g_portable.load(std::memory_order_relaxed)) {
+        sha256_shani(state, p, blocks);
+        return;
+    }
+#endif
+    sha256_portable(state, p, blocks);
+}
+
+void sha256_init(Sha256State& s) {
+    std::memcpy(s.h, kIV, sizeof(kIV));
+    std::memset(s.buf, 0, sizeof(s.buf));
+    s.fill = 0;
+    s.bits = 0;
+}
+
+void sha256_update(Sha256State& s, const std::uint8_t* p, std::size_t n) {
+    if (!n) return;
+    s.bits += (std::uint64_t)n * 8u;
+    if (s.fill) {
+        const std::size_t m = n < 64 - s.fill ? n : 64 - s.fill;
+        std::memcpy(s.buf + s.fill, p, m);
+        s.fill += m;
+        p += m;
+        n -= m;
+        if (s.fill < 64) return;
+        sha256_blocks(s.h, s.buf, 1);
+        s.fill = 0;
+    }
+    const std::size_t whole = n / 64;
+    sha256_blocks(s.h, p, whole);
+    p += 64 * whole;
+    n -= 64 * whole;
+    if (n) std::memcpy(s.buf, p, n);
+    s.fill = n;
+}
+
+std::array<std::uint8_t, 32> sha256_final(Sha256State& s) {
+    const std::uint64_t bits = s.bits;
+    std::uint8_t pad[128] = {0x80};
+    const std::size_t padlen = (s.fill < 56 ? 56 - s.fill : 120 - s.fill);
+    for (int i = 0; i < 8; ++i) pad[padlen + i] = (std::uint8_t)(bits >> (56 - 8 * i));
+    // the length bytes must not count toward the length: feed through the buffer directly
+    std::size_t n = padlen + 8, off = 0;
+    while (n) {
+        const std::size_t m = n < 64 - s.fill ? n : 64 - s.fill;
+        std::memcpy(s.buf + s.fill, pad + off, m);
+        s.fill += m;
+        off += m;
+        n -= m;
+        if (s.fill == 64) {
+            sha256_blocks(s.h, s.buf, 1);
+            s.fill = 0;
+        }
+    }
+    std::array<std::uint8_t, 32> d{};
+    for (int i = 0; i < 8; ++i)
+        for (int b = 0; b < 4; ++b) d[4 * i + b] = (std::uint8_t)(s.h[i] >> (24 - 8 * b));
+    sha256_init(s);  // finalize resets the hasher (Sha256.cpp:122-124)
+    return d;
+}
+
+std::array<std::uint8_t, 32> sha256(const std::uint8_t* p, std::size_t n) {
+    Sha256State s;
+    sha256_init(s);
+    sha256_update(s, p, n);
+    return sha256_final(s);
+}
+
+std::array<std::uint8_t, 32> hmac_sha256(const std::uint8_t* key, std::size_t key_len,
+                                         const std::uint8_t* data, std::size_t n) {
+    std::uint8_t k[64] = {0};
+    if (key_len > 64) {
+        const auto kh = sha256(key, key_len);
+        std::memcpy(k, kh.data(), 32);
+    } else if (key_len) {
+        std::memcpy(k, key, key_len);
+    }
+    std::uint8_t pad[64];
+    Sha256State s;
+    sha256_init(s);
+    for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x36u;
+    sha256_update(s, pad, 64);
+    sha256_update(s, data, n);
+    const auto inner = sha256_final(s);
+    for (int i = 0; i < 64; ++i) pad[i] = k[i] ^ 0x5cu;
+    sha256_update(s, pad, 64);
+    sha256_update(s, inner.data(), 32);
+    volatile std::uint8_t* vk = k;
+    for (int i = 0; i < 64; ++i) vk[i] = 0;
+    return sha256_final(s);
+}
+
+void chacha20_xor(const std::uint8_t key[32], const std::uint8_t nonce[12], std::uint32_t counter,
+                  const std::uint8_t* in, std::uint8_t* out, std::size_t n) {
+    if (!n) return;
+    std::uint32_t s[16];
+    for (int i = 0; i < 4; ++i) s[i] = kSigma[i];
+    for (int i = 0; i < 8; ++i) s[4 + i] = le32(key + 4 * i);
+    s[12] = counter;
+    for (int i = 0; i < 3; ++i) s[13 + i] = le32(nonce + 4 * i);
+#if defined(__x86_64__)
+    if (have_avx2() && !g_portable.load(std::memory_order_relaxed) && n >= 512) {
+        const std::size_t n8 = n / 512;
+        chacha_avx2(s, in, out, n8);
+        in += 512 * n8;
+        out += 512 * n8;
+        n -= 512 * n8;
+    }
+#endif
+    chacha_portable(s, in, out, n);
+    std::memset(s, 0, sizeof(s));
+}
+
+void pow_prefix(PowPrefix& pp, const std::uint8_t* prefix, std::size_t n) {
+    std::memcpy(pp.mid, kIV, sizeof(kIV));
+    const std::size_t whole = n / 64;
+    sha256_blocks(pp.mid, prefix, whole);
+    pp.tail_len = n - 64 * whole;
+    std::memset(pp.tail, 0, sizeof(pp.tail));
+    if (pp.tail_len) std::memcpy(pp.tail, prefix + 64 * whole, pp.tail_len);
+    pp.total_len = n;
+}
+
+std::array<std::uint8_t, 32> pow_digest(const PowPrefix& pp, std::uint64_t nonce) {
+    std::uint8_t blk[128] = {0};
+    std::memcpy(blk, pp.tail, pp.tail_len);
+    for (int i = 0; i < 8; ++i) blk[pp.tail_len + i] = (std::uint8_t)(nonce >> (56 - 8 * i));
+    const std::size_t m = pp.tail_len + 8;
+    blk[m] = 0x80;
+    const std::size_t nb = m + 9 <= 64 ? 1 : 2;
+    const std::uint64_t bits = (pp.total_len + 8) * 8u;
+    for (int i = 0; i < 8; ++i) blk[64 * nb - 8 + i] = (std::uint8_t)(bits >> (56 - 8 * i));
+    std::uint32_t st[8];
+    std::memcpy(st, pp.mid, sizeof(st));
+    sha256_blocks(st, blk, nb);
+    std::array<std::uint8_t, 32> d{};
+    for (int i = 0; i < 8; ++i)
+        for (int b = 0; b < 4; ++b) d[4 * i + b] = (std::uint8_t)(st[i] >> (24 - 8 * b));
+    return d;
+}
+
+unsigned leading_zero_bits(const std::array<std::uint8_t, 32>& d) {
+    unsigned total = 0;
+    for (const std::uint8_t b : d) {
+        if (b == 0) {
+            total += 8;
+            continue;
+        }
+        return total + (unsigned)__builtin_clz((unsigned)b) - 24u;
+    }
+    return total;
+}
+
+}  // namespace enet::host

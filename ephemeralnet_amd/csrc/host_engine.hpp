@@ -1,0 +1,71 @@
+// host_engine.hpp -- the scalar host engine: SHA-256 / HMAC-SHA256 / ChaCha20 for ONE record on
+// the calling CPU thread (SHA-NI and AVX2 when the CPU has them, portable code otherwise).
+//
+// Why it exists: the reference API is per record and is called from many
+// session threads (SessionManager.cpp:332,703), and a GPU round trip costs >= ~18 us before any
+// byte moves.  SHA-256 of one message is a serial Merkle-Damgard chain (one GPU lane runs it
+// ~16x slower than a core), and a 98-byte HMAC or a 1500-byte frame is done on a core in about a
+// microsecond.  So the scalar C++ drop-in (crypto_api.cpp) runs serial and small work here and
+// sends only large ChaCha20 calls -- coalesced across threads -- and every batch entry point to
+// the MI355X.  This is a first-class path chosen by size, not a fallback of the GPU kernels: the
+// C ABI's batch entry points never come here.  It is the builder's own code (RFC 8439 / FIPS
+// 180-4 / RFC 2104); nothing from oracle/ or the reference is linked (tests/test_boundary.py).
+//
+// Semantics restated (ShardianLabs/EphemeralNet):
+//   ChaCha20::apply   src/crypto/ChaCha20.cpp:98-121 (u32 counter wrap :110, keystream wiped)
+//   Sha256            src/crypto/Sha256.cpp:66-176
+//   HmacSha256        src/crypto/HmacSha256.cpp:11-54 (keys > 64 B hashed first, :15-17)
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+
+namespace enet::host {
+
+// FIPS 180-4 initial hash value
+inline constexpr std::uint32_t kIV[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                                         0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+
+// `blocks` 64-byte blocks at p into state (SHA-NI when available)
+void sha256_blocks(std::uint32_t state[8], const std::uint8_t* p, std::size_t blocks);
+
+// Streaming SHA-256 with a 64-byte buffer (the reference's Sha256 member layout)
+struct Sha256State {
+    std::uint32_t h[8];
+    std::uint8_t buf[64];
+    std::size_t fill;
+    std::uint64_t bits;
+};
+void sha256_init(Sha256State& s);
+void sha256_update(Sha256State& s, const std::uint8_t* p, std::size_t n);
+std::array<std::uint8_t, 32> sha256_final(Sha256State& s);  // resets s
+std::array<std::uint8_t, 32> sha256(const std::uint8_t* p, std::size_t n);
+
+// RFC 2104 with the reference's key handling (HmacSha256.cpp:11-39)
+std::array<std::uint8_t, 32> hmac_sha256(const std::uint8_t* key, std::size_t key_len,
+                                         const std::uint8_t* data, std::size_t n);
+
+// out[0..n) = in[0..n) XOR ChaCha20 keystream (key, nonce) from block `counter` (u32 wrap).
+// in == out is allowed.
+void chacha20_xor(const std::uint8_t key[32], const std::uint8_t nonce[12], std::uint32_t counter,
+                  const std::uint8_t* in, std::uint8_t* out, std::size_t n);
+
+// SHA-256(prefix || BE64(nonce)) leading zero bits >= difficulty (StoreProof.cpp:47-69,
+// Node.cpp:174-205); the prefix midstate is computed once per search
+struct PowPrefix {
+    std::uint32_t mid[8];        // state after the prefix's whole 64-byte blocks
+    std::uint8_t tail[64];       // the remaining prefix bytes
+    std::size_t tail_len;
+    std::uint64_t total_len;     // prefix bytes
+};
+void pow_prefix(PowPrefix& pp, const std::uint8_t* prefix, std::size_t n);
+std::array<std::uint8_t, 32> pow_digest(const PowPrefix& pp, std::uint64_t nonce);
+unsigned leading_zero_bits(const std::array<std::uint8_t, 32>& d);
+
+// Which implementations this CPU runs ("sha-ni+avx2", "portable", ...), for reports.
+const char* isa();
+// Force the portable code (tests compare both; 0 = auto)
+void force_portable(bool on);
+
+}  // namespace enet::host

@@ -99,7 +99,7 @@ __device__ __forceinline__ uint32_t slab_sw(uint32_t o) { return ((o >> 1) & 7u)
 
 constexpr uint32_t kStage = 2;                 // blocks per lane per cooperative stage
 constexpr uint32_t kRun = 64 * kStage;         // bytes per owner per stage
-constexpr uint32_t kRing = 272;                // COOP 4: two-line ring (256 B) + 16 B pad per owner
+constexpr uint32_t kRing = 288;                // COOP 4: two-line ring (256 B) + 32 B pad per owner
 
 // Streaming output store: the kernel never reads its outputs back, so stores that fill whole
 // 128-byte lines are non-temporal (global_store ... nt) instead of being kept dirty in the per-XCD
@@ -482,7 +482,19 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         const uint32_t lane = threadIdx.x & 63u;
         const uint32_t wbase = threadIdx.x & ~63u;
         const uint32_t Lu = (uint32_t)p.uniform_len;
-        const uint32_t kk = lane & 7u;
+        // load / store roles: instruction i serves owner 8i + rq with its 16-byte chunk rc, each
+        // quad of lanes one aligned 64-byte half line (whole lines per instruction, as before).
+        // The quad -> (owner, half) map below makes the ring's ds_read_b128 lane groups
+        // ({0-3,12-15,20-27}, ...; bank = dword mod 64) and the ds_write_b128 8-lane groups
+        // (bank = dword mod 32) conflict-free with the 72-dword ring stride (kRing = 288 B): the
+        // identity map (owner = lane / 8, chunk = lane % 8) left every ds_read_b128 2- to 3-way
+        // conflicted (PMC 12.3 M conflict cycles per C3 launch, profiles/pmc_c3_r02.json) and no
+        // stride <= 88 dwords is conflict-free with it.  The run's own dword accesses
+        // (ring_at: ds_read/write_b32, bank = dword mod 32) stay conflict-free when
+        // 72 + L/4 is odd (C3: L = 1500).
+        const uint32_t rk = lane >> 2;
+        const uint32_t rq = 2u * ((rk >> 1) & 3u) + (rk >> 3);
+        const uint32_t rc = 4u * ((rk ^ (rk >> 1) ^ (rk >> 2)) & 1u) + (lane & 3u);
         const uint32_t wgid0 = blockIdx.x * WGS + wbase;
         const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
         uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
@@ -499,12 +511,11 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         // for arenas < 4 GiB)
         const uint8_t* ial = ibase - (ib & 127u);
         uint8_t* oal = obase - (ib & 127u);
-        // load / store roles: instruction i serves owner o = 8i + lane/8, 16-byte chunk kk
         uint32_t roff[8];  // line 0 of owner o
         uint32_t rgeo[8];  // d | lines << 8 | end-bytes-in-last-line << 16
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const uint32_t o = 8u * i + (lane >> 3);
+            const uint32_t o = 8u * i + rq;
             const uint32_t g = wgid0 + o;
             const uint32_t d = (ib + g * Lu) & 127u;
             roff[i] = g * Lu + (ib & 127u) - d;
@@ -517,7 +528,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (t < ((rgeo[i] >> 8) & 0xffu)) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(ial + (roff[i] + 128u * t + 16u * kk));
+                    const uint4 v = *reinterpret_cast<const uint4*>(ial + (roff[i] + 128u * t + 16u * rc));
                     pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
                 }
             }
@@ -525,15 +536,15 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         auto land = [&](uint32_t t) {  // pf -> ring slot t % 2 of every role owner
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                *reinterpret_cast<uint4*>(wslab + (8u * i + (lane >> 3)) * kRing + 128u * (t & 1u) + 16u * kk) =
+                *reinterpret_cast<uint4*>(wslab + (8u * i + rq) * kRing + 128u * (t & 1u) + 16u * rc) =
                     make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
         };
         auto store_inner = [&](uint32_t t) {  // line t, 1 <= t <= S-2: complete in every record
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                store_stream(oal + (roff[i] + 128u * t + 16u * kk),
-                             *reinterpret_cast<const uint4*>(wslab + (8u * i + (lane >> 3)) * kRing +
-                                                             128u * (t & 1u) + 16u * kk));
+                store_stream(oal + (roff[i] + 128u * t + 16u * rc),
+                             *reinterpret_cast<const uint4*>(wslab + (8u * i + rq) * kRing +
+                                                             128u * (t & 1u) + 16u * rc));
         };
         auto store_line = [&](uint32_t t) {  // ring slot t % 2 -> line t, this record's bytes only
 #pragma unroll
@@ -541,10 +552,10 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
                 const uint32_t d = rgeo[i] & 0xffu, nl = (rgeo[i] >> 8) & 0xffu, e = rgeo[i] >> 16;
                 if (t >= nl) continue;
                 const uint32_t lo = t == 0 ? d : 0u, hi = t + 1 == nl ? e : 128u;
-                const uint32_t c0 = 16u * kk;
+                const uint32_t c0 = 16u * rc;
                 if (c0 + 16u <= lo || c0 >= hi) continue;
                 const uint4 v = *reinterpret_cast<const uint4*>(
-                    wslab + (8u * i + (lane >> 3)) * kRing + 128u * (t & 1u) + c0);
+                    wslab + (8u * i + rq) * kRing + 128u * (t & 1u) + c0);
                 uint8_t* q = oal + (roff[i] + 128u * t + c0);
                 if (c0 >= lo && c0 + 16u <= hi) {
                     store_stream(q, v);

@@ -268,6 +268,52 @@ ENET_API int enet_set_lanes_per_record(uint32_t lanes);
  * keystream block (four waves per SIMD), 0 = per-lane path only, -1 restores the default.
  * Results are identical; tuning / test knob. */
 ENET_API int enet_set_staging(int variant);
+/* ---- scalar C++ drop-in routing (include/ephemeralnet/crypto/{ChaCha20,Sha256,HmacSha256,
+ *      CryptoManager}.hpp, security/StoreProof.hpp, network/KeyManager.hpp)
+ * The reference signatures take ONE record per call from many session threads
+ * (SessionManager.cpp:332,703) and never throw.  A GPU round trip costs >= ~18 us,
+ * and SHA-256 of one message is one serial chain, so the drop-in routes each call by size:
+ *   ENET_SCALAR_AUTO (default)  SHA-256 / HMAC / single PoW checks and ChaCha20 records below the
+ *                               crossover run on the calling thread's host engine (SHA-NI / AVX2,
+ *                               csrc/host_engine.cpp); ChaCha20 records at or above it go to the
+ *                               MI355X, concurrent callers coalesced into one launch; PoW
+ *                               searches and KeyManager::rotate_all_due run on the MI355X.
+ *   ENET_SCALAR_DEVICE          every call that has a device kernel runs on the MI355X (round-2
+ *                               behaviour; the streaming Sha256 class stays on the host).
+ *   ENET_SCALAR_HOST            everything on the host engine.
+ * crossover_bytes = 0 keeps the current value (default 262144).  A failed device call of the
+ * scalar API is finished on the host engine (bit-exact), counted in device_failures and reported
+ * once on stderr -- or, after enet_scalar_set_on_device_error(1), abort()s.  No exception ever
+ * leaves a reference signature except std::bad_alloc.  The batch entry points (this header's
+ * *_batch / pipeline calls and C++ crypto::batch::*) never use the host engine. */
+#define ENET_SCALAR_AUTO 0
+#define ENET_SCALAR_DEVICE 1
+#define ENET_SCALAR_HOST 2
+ENET_API int enet_scalar_set_policy(int policy, uint64_t crossover_bytes);
+ENET_API int enet_scalar_policy(void);
+/* 0 = finish a failed device call on the host engine (default), 1 = abort() */
+ENET_API int enet_scalar_set_on_device_error(int mode);
+typedef struct enet_scalar_stats {
+    uint64_t host_calls;         /* scalar calls served by the host engine */
+    uint64_t device_calls;       /* scalar calls served by the MI355X */
+    uint64_t device_failures;    /* device calls that failed and were finished on the host */
+    uint64_t coalesced_launches; /* device launches of the ChaCha20::apply coalescer */
+    uint64_t coalesced_records;  /* records they carried (>= launches: calls merged across threads) */
+} enet_scalar_stats;
+ENET_API void enet_scalar_get_stats(enet_scalar_stats* out);
+ENET_API void enet_scalar_reset_stats(void);
+/* Test hook: the next n device calls of the scalar API fail as if the device had. */
+ENET_API void enet_scalar_inject_device_failures(uint32_t n);
+/* The host engine's instruction sets on this CPU ("sha-ni+avx2", ..., "portable"). */
+ENET_API const char* enet_host_isa(void);
+/* The host engine itself, one record (host pointers): ChaCha20::apply, Sha256::digest,
+ * HmacSha256::compute semantics.  For callers that want the scalar path without the C++ API. */
+ENET_API void enet_host_chacha20_xor(const uint8_t key[32], const uint8_t nonce[12], uint32_t counter,
+                                     const uint8_t* in, uint8_t* out, uint64_t n);
+ENET_API void enet_host_sha256(const uint8_t* in, uint64_t n, uint8_t digest[32]);
+ENET_API void enet_host_hmac_sha256(const uint8_t* key, uint64_t key_len, const uint8_t* in, uint64_t n,
+                                    uint8_t mac[32]);
+
 /* Human-readable text of the last error on this host thread ("" if none). */
 ENET_API const char* enet_last_error(void);
 /* ABI version: (major << 16) | minor. */

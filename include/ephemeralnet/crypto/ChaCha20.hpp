@@ -1,5 +1,6 @@
 // ChaCha20.hpp -- drop-in for the reference include/ephemeralnet/crypto/ChaCha20.hpp:10-24.
-// Same types and signature; the keystream runs on the MI355X (libenet_crypto.so).
+// Same types and signature.  Records below the scalar crossover run on the host engine, larger
+// ones on the MI355X, concurrent callers coalesced into one launch (enet_crypto.h "scalar").
 #pragma once
 
 #include <array>
@@ -22,7 +23,7 @@ struct Nonce {
 class ENET_CXX_API ChaCha20 {
 public:
     // ChaCha20.cpp:98-121: output.resize(input.size()); output = input XOR keystream starting at
-    // `counter` (uint32, wraps mod 2^32).  Throws std::runtime_error if the GPU path fails.
+    // `counter` (uint32, wraps mod 2^32).  Never throws (except std::bad_alloc), like the reference.
     static void apply(const Key& key,
                       const Nonce& nonce,
                       std::span<const std::uint8_t> input,

@@ -232,6 +232,37 @@ int main() {
         } else if (op == "chunk_id") {
             std::string d; in >> d;
             std::cout << hex(security::derive_chunk_id(unhex(d))) << "\n";
+        } else if (op == "policy") {
+            // scalar routing: auto | device | host [crossover bytes]
+            std::string pol; uint64_t cross = 0;
+            in >> pol >> cross;
+            const int pv = pol == "device" ? ENET_SCALAR_DEVICE : pol == "host" ? ENET_SCALAR_HOST : ENET_SCALAR_AUTO;
+            std::cout << enet_scalar_set_policy(pv, cross) << "\n";
+        } else if (op == "stats") {
+            enet_scalar_stats st{};
+            enet_scalar_get_stats(&st);
+            std::cout << st.host_calls << " " << st.device_calls << " " << st.device_failures << " "
+                      << st.coalesced_launches << " " << st.coalesced_records << "\n";
+        } else if (op == "reset_stats") {
+            enet_scalar_reset_stats();
+            std::cout << "ok\n";
+        } else if (op == "inject") {
+            uint32_t n = 0; in >> n;
+            enet_scalar_inject_device_failures(n);
+            std::cout << "ok\n";
+        } else if (op == "isa") {
+            std::cout << enet_host_isa() << "\n";
+        } else if (op == "chacha_inplace") {
+            // ChaCha20::apply with the input span aliasing the output vector (reference callers may)
+            std::string k, n, c, p;
+            in >> k >> n >> c >> p;
+            crypto::Key key; crypto::Nonce nonce;
+            auto kb = unhex(k), nb = unhex(n);
+            std::copy(kb.begin(), kb.end(), key.bytes.begin());
+            std::copy(nb.begin(), nb.end(), nonce.bytes.begin());
+            std::vector<uint8_t> buf = unhex(p);
+            crypto::ChaCha20::apply(key, nonce, buf, buf, (uint32_t)std::stoul(c));
+            std::cout << hex(buf) << "\n";
         } else if (!op.empty()) {
             std::cout << "?\n";
         }

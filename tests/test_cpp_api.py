@@ -34,15 +34,19 @@ def test_cpp_api_compiles_and_links(api_bin):
     assert os.access(api_bin, os.X_OK)
 
 
-@pytest.mark.gpu
-def test_cpp_api_matches_reference_golden(api_bin, golden):
+def scalar_ops(golden, big=False):
+    """Reference-signature calls (ChaCha20::apply, Sha256, HmacSha256, CryptoManager) with the
+    golden answers of the compiled reference.  big: also the records over 4 KiB (64 KiB)."""
     ops, expect = [], []
     for c in golden["chacha20"]:
-        if c["len"] > 4097:
+        if c["len"] > 4097 and not big:
             continue
         pt = splitmix_bytes(c["pt_seed"], c["len"])
         ops.append(f"chacha {c['key']} {c['nonce']} {c['counter']} {h(pt)}")
         expect.append(("hex", c["ct"]))
+        if c["len"] <= 4097:
+            ops.append(f"chacha_inplace {c['key']} {c['nonce']} {c['counter']} {h(pt)}")
+            expect.append(("hex", c["ct"]))
     for c in golden["sha256"]:
         data = b"abc" if c["abc"] else splitmix_bytes(c["seed"], c["len"])
         ops.append(f"sha {h(data)}")
@@ -50,6 +54,8 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         if c["digest_pieces_7"]:
             ops.append(f"sha_pieces 7 {h(data)}")
             expect.append(("eq", c["digest_pieces_7"]))
+            ops.append(f"sha_pieces 64 {h(data)}")
+            expect.append(("eq", c["digest"]))
     for c in golden["hmac"]:
         ops.append(f"hmac {c['key'] or '-'} {h(splitmix_bytes(c['seed'], c['len']))}")
         expect.append(("eq", c["mac"]))
@@ -57,10 +63,9 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         ops.append(f"hverify {c['key']} {h(splitmix_bytes(c['seed'], c['len']))} {c['mac']}")
         expect.append(("eq", "1" if c["ok"] else "0"))
     for c in golden["cryptomanager"]:
-        if c["len"] > 4097:
+        if c["len"] > 4097 and not big:
             continue
         pt = splitmix_bytes(c["pt_seed"], c["len"])
-        import oracle
         ct = oracle.chacha20_xor(bytes.fromhex(c["key"]), bytes.fromhex(c["nonce"]), pt,
                                  oracle.derive_counter(bytes.fromhex(c["chunk_id"])))
         assert ("hex" not in c["ct"]) or ct.hex() == c["ct"]["hex"]
@@ -68,26 +73,20 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         expect.append(("eq", h(pt)))
         ops.append(f"cm_roundtrip {c['chunk_id']} {h(pt)}")
         expect.append(("eq", "1"))
-    for f in golden["frames"]:
-        m = bytes.fromhex(f["signed"])[:-32]
-        ops.append(f"frame_seal {f['key']} {f['nonce']} {h(m)}")
-        expect.append(("eq", f"{f['body']} 1"))
-    for f in golden["frames"]:
-        m = bytes.fromhex(f["signed"])[:-32]
-        ops.append(f"wire_queue {f['key']} {h(m)}")
-        expect.append(("wire", (bytes.fromhex(f["key"]), m)))
-    for L in (0, 1, 64, 1500, 4096):
-        pt = splitmix_bytes(777 + L, L)
-        ops.append(f"chunk_pipe {h(pt)}")
-        expect.append(("eq", f"{hashlib.sha256(pt).hexdigest()} 1"))
-    for c in golden["aead"]:
-        if c["aad_len"] or c["len"] > 1500:
-            continue
-        pt = splitmix_bytes(c["pt_seed"], c["len"])
-        ops.append(f"aead_seal {c['key']} {c['nonce']} {h(pt)}")
-        expect.append(("eq", f"{c['ct']['hex'] or '-'} {c['tag']}"))
+    for L in (0, 1, 4096):
+        d = splitmix_bytes(40000 + L, L)
+        ops.append(f"chunk_id {h(d)}")
+        expect.append(("eq", hashlib.sha256(d).hexdigest()))
+    return ops, expect
+
+
+def run_ops(api_bin, ops):
     res = subprocess.run([api_bin], input="\n".join(ops) + "\n", capture_output=True, text=True,
-                         check=True, timeout=300).stdout.splitlines()
+                         check=True, timeout=300)
+    return res.stdout.splitlines(), res.stderr
+
+
+def check(ops, expect, res):
     assert len(res) == len(ops)
     for op, (kind, e), got in zip(ops, expect, res):
         if kind == "hex":
@@ -106,10 +105,86 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
             assert got == e, op[:60]
 
 
+def stats(line):
+    host, dev, fail, launches, records = map(int, line.split())
+    return {"host": host, "device": dev, "failures": fail, "launches": launches, "records": records}
+
+
+@pytest.mark.parametrize("policy", ["host", "auto"])
+def test_cpp_scalar_api_host_engine_golden(api_bin, golden, policy):
+    """CPU, no GPU: the reference signatures served by the host engine (SHA-NI / AVX2 or portable)
+    reproduce the compiled reference's golden vectors, including streaming Sha256 in 7- and
+    64-byte pieces and in-place ChaCha20::apply; every call is counted on the host."""
+    ops, expect = scalar_ops(golden, big=True)
+    res, _ = run_ops(api_bin, [f"policy {policy}", "reset_stats"] + ops + ["stats"])
+    assert res[:2] == ["0", "ok"]
+    check(ops, expect, res[2:-1])
+    st = stats(res[-1])
+    assert st["host"] > 0 and st["device"] == 0 and st["failures"] == 0
+
+
+def test_cpp_scalar_api_device_failure_finishes_on_host(api_bin, golden):
+    """Injected failure on the CPU build: ENET_SCALAR_DEVICE with no usable
+    device -- every device call fails, is counted, reported once on stderr, and finished on the
+    host engine bit-exactly; nothing throws into the caller (the process exits 0)."""
+    ops, expect = scalar_ops(golden)
+    res, err = run_ops(api_bin, ["policy device", "reset_stats"] + ops + ["stats"])
+    check(ops, expect, res[2:-1])
+    st = stats(res[-1])
+    assert st["failures"] > 0 and st["device"] == 0 and st["host"] >= st["failures"]
+    assert err.count("finished on the host engine") == 1
+
+
 @pytest.mark.gpu
-def test_cpp_pow_and_keys_match_reference_golden(api_bin):
-    """security::StoreProof, crypto::batch PoW (Node.cpp announce / handshake) and
-    network::KeyManager through the reference C++ signatures against tests/golden/pow.json."""
+def test_cpp_api_matches_reference_golden(api_bin, golden):
+    ops, expect = scalar_ops(golden, big=True)
+    for f in golden["frames"]:
+        m = bytes.fromhex(f["signed"])[:-32]
+        ops.append(f"frame_seal {f['key']} {f['nonce']} {h(m)}")
+        expect.append(("eq", f"{f['body']} 1"))
+    for f in golden["frames"]:
+        m = bytes.fromhex(f["signed"])[:-32]
+        ops.append(f"wire_queue {f['key']} {h(m)}")
+        expect.append(("wire", (bytes.fromhex(f["key"]), m)))
+    for L in (0, 1, 64, 1500, 4096):
+        pt = splitmix_bytes(777 + L, L)
+        ops.append(f"chunk_pipe {h(pt)}")
+        expect.append(("eq", f"{hashlib.sha256(pt).hexdigest()} 1"))
+    for c in golden["aead"]:
+        if c["aad_len"] or c["len"] > 1500:
+            continue
+        pt = splitmix_bytes(c["pt_seed"], c["len"])
+        ops.append(f"aead_seal {c['key']} {c['nonce']} {h(pt)}")
+        expect.append(("eq", f"{c['ct']['hex'] or '-'} {c['tag']}"))
+    # every policy: the device (each call one GPU round trip), auto with a 1-byte crossover (every
+    # ChaCha20 record through the coalescer), the default auto and the host engine
+    for pol in ("policy device", "policy auto 1", "policy auto 262144", "policy host"):
+        res, err = run_ops(api_bin, [pol, "reset_stats"] + ops + ["stats"])
+        assert res[:2] == ["0", "ok"], pol
+        check(ops, expect, res[2:-1])
+        st = stats(res[-1])
+        assert st["failures"] == 0, (pol, err)
+        if pol == "policy device":
+            assert st["device"] > 0
+        if pol == "policy auto 1":
+            assert st["launches"] > 0 and st["records"] >= st["launches"]
+
+
+@pytest.mark.gpu
+def test_cpp_scalar_device_failure_injected_on_gpu(api_bin, golden):
+    """On the GPU box: the next 5 device calls fail (enet_scalar_inject_device_failures); those
+    calls are finished on the host engine with the same bytes, later calls use the device."""
+    ops, expect = scalar_ops(golden)
+    res, err = run_ops(api_bin, ["policy device", "reset_stats", "inject 5"] + ops + ["stats"])
+    check(ops, expect, res[3:-1])
+    st = stats(res[-1])
+    assert st["failures"] == 5 and st["device"] > 0
+    assert err.count("finished on the host engine") == 1
+
+
+def pow_ops(batch=True):
+    """security::StoreProof, network::KeyManager (and with batch=True the crypto::batch PoW
+    searches of Node.cpp announce / handshake) against tests/golden/pow.json."""
     import json
     with open(os.path.join(ROOT, "tests", "golden", "pow.json")) as f:
         pg = json.load(f)
@@ -120,16 +195,17 @@ def test_cpp_pow_and_keys_match_reference_golden(api_bin):
         ops.append(f"store_pow {c['chunk_id']} {c['payload_size']} {c['hint'] or '-'} {c['difficulty']} "
                    f"{c['max_attempts']}")
         expect.append(f"{c['nonce']} {int(c['valid'])} {int(c['valid_next'])}" if c["found"] else "none")
-    for c in pg["handshake_pow"]:
-        ops.append(f"handshake_pow {c['initiator']} {c['responder']} {c['public']} {c['difficulty']}")
-        dn = c["nonce"] if c["found"] else 2**64 - 1  # Node.cpp drop-in: nonce_out untouched if not found
-        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} 1 {int(c['found'])} {dn}")
-    for c in pg["announce_pow"]:
-        ops.append("announce_pow " + " ".join(c[k] or "-" for k in ("chunk_id", "peer_id", "endpoint",
-                                                                   "manifest_uri", "assigned_shards"))
-                   + f" {c['ttl']} {c['difficulty']}")
-        dn = c["nonce"] if c["found"] else 2**64 - 1
-        expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} {int(c['found'])} {dn}")
+    if batch:
+        for c in pg["handshake_pow"]:
+            ops.append(f"handshake_pow {c['initiator']} {c['responder']} {c['public']} {c['difficulty']}")
+            dn = c["nonce"] if c["found"] else 2**64 - 1  # Node.cpp drop-in: nonce_out untouched if not found
+            expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} 1 {int(c['found'])} {dn}")
+        for c in pg["announce_pow"]:
+            ops.append("announce_pow " + " ".join(c[k] or "-" for k in ("chunk_id", "peer_id", "endpoint",
+                                                                       "manifest_uri", "assigned_shards"))
+                       + f" {c['ttl']} {c['difficulty']}")
+            dn = c["nonce"] if c["found"] else 2**64 - 1
+            expect.append(f"{int(c['found'])} {c['nonce']} {c['attempt']} {int(c['found'])} {dn}")
     for c in pg["session_keys"]:
         ops.append(f"keymgr {c['secret']} {c['material']} {c['rotate_ticks']}")
         expect.append(f"{c['material_key']} {c['rotated_key']} 1")
@@ -140,8 +216,31 @@ def test_cpp_pow_and_keys_match_reference_golden(api_bin):
         d = splitmix_bytes(40000 + L, L)
         ops.append(f"chunk_id {h(d)}")
         expect.append(hashlib.sha256(d).hexdigest())
-    res = subprocess.run([api_bin], input="\n".join(ops) + "\n", capture_output=True, text=True,
-                         check=True, timeout=300).stdout.splitlines()
-    assert len(res) == len(ops)
-    for op, e, got in zip(ops, expect, res):
+    return ops, expect
+
+
+def test_cpp_storeproof_and_keys_host_engine_golden(api_bin):
+    """CPU: compute_store_pow / store_pow_valid (StoreProof.cpp), KeyManager (KeyManager.cpp) and
+    derive_chunk_id through the reference signatures on the host engine -- the reference's own
+    golden answers (tests/golden/pow.json)."""
+    ops, expect = pow_ops(batch=False)
+    res, _ = run_ops(api_bin, ["policy host"] + ops)
+    assert res[0] == "0"
+    assert len(res) == len(ops) + 1
+    for op, e, got in zip(ops, expect, res[1:]):
         assert got == e, op[:80]
+
+
+@pytest.mark.gpu
+def test_cpp_pow_and_keys_match_reference_golden(api_bin):
+    """security::StoreProof, crypto::batch PoW (Node.cpp announce / handshake) and
+    network::KeyManager through the reference C++ signatures against tests/golden/pow.json, on
+    the device (policy device and the default auto)."""
+    ops, expect = pow_ops()
+    for pol in ("policy device", "policy auto"):
+        res, err = run_ops(api_bin, [pol, "reset_stats"] + ops + ["stats"])
+        assert len(res) == len(ops) + 3
+        for op, e, got in zip(ops, expect, res[2:-1]):
+            assert got == e, (pol, op[:80])
+        st = stats(res[-1])
+        assert st["failures"] == 0 and st["device"] > 0, (pol, err)

@@ -195,6 +195,55 @@ def test_frames_invalid_geometry(enet):
         assert (ok[i], got[i]) == ((0, bytes(L - 1)) if i == 9 else (1, msgs[i])), i
 
 
+def test_frames_decreasing_offsets(enet):
+    """Output offsets that DECREASE (out_off[k+1] < out_off[k]) must not wrap the record length:
+    record k is skipped (nothing written for it), the records whose range is merely the wrong
+    size are zeroed as usual, and everything else -- including the guard bytes past the arena --
+    is untouched (Lo was never bounds-checked)."""
+    import torch
+    n, L = 300, 500
+    msgs = [splitmix_bytes(44000 + i, L) for i in range(n)]
+    keys = [splitmix_bytes(45000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(46000 + i, 12) for i in range(n)]
+    b = enet.make_batch(msgs, keys, nonces)
+    ooffs = offsets_for([L + 32] * n, 0)
+    ooffs[11] = ooffs[10] - 5          # record 10: end < start; record 11: too long
+    total = int(ooffs[-1])
+    out = torch.full((total + 4096,), 0x5A, dtype=torch.uint8, device="cuda")
+    enet.frame_seal(b, out, torch.tensor(ooffs).cuda())
+    ob = host(out)
+    assert ob[total:] == b"\x5a" * 4096
+    for i in range(n):
+        if i in (10, 11):
+            continue
+        want = oracle.frame_seal(keys[i], nonces[i], msgs[i])
+        if i == 9:  # record 11's zeroed range starts 5 bytes inside record 9
+            assert ob[ooffs[9]:ooffs[10] - 5] == want[:-5]
+            continue
+        assert ob[ooffs[i]:ooffs[i + 1]] == want, i
+    # (its first 5 bytes are also record 9's last 5: either writer may land last)
+    assert ob[ooffs[11] + 5:ooffs[12]] == bytes(int(ooffs[12] - ooffs[11] - 5))
+    # open with a decreasing pair: ok = 0 for the disordered record, nothing written past the arena
+    good = [oracle.frame_seal(keys[i], nonces[i], msgs[i]) for i in range(n)]
+    bw = enet.make_batch(good, keys, nonces)
+    poffs = offsets_for([L] * n, 0)
+    poffs[21] = poffs[20] - 3
+    pt = torch.full((int(poffs[-1]) + 4096,), 0xAA, dtype=torch.uint8, device="cuda")
+    macs = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    ok = torch.full((n,), 7, dtype=torch.uint8, device="cuda")
+    enet.frame_open(bw, pt, torch.tensor(poffs).cuda(), macs, ok)
+    okl = ok.cpu().tolist()
+    pb = host(pt)
+    assert pb[int(poffs[-1]):] == b"\xaa" * 4096
+    for i in range(n):
+        if i in (20, 21):
+            assert okl[i] == 0, i
+        elif i == 19:  # record 21's zeroed range starts 3 bytes inside record 19
+            assert okl[i] == 1 and pb[poffs[19]:poffs[20] - 3] == msgs[19][:-3]
+        else:
+            assert okl[i] == 1 and pb[poffs[i]:poffs[i + 1]] == msgs[i], i
+
+
 @pytest.mark.parametrize("n,L", [(1 << 20, 1500)])
 def test_wire_frames_full_c3_roundtrip(enet, n, L):
     """C3 at full size (1 M x 1500 B MTU frames -> 1548-byte wire frames): open(seal(m)) == m with
