@@ -42,25 +42,27 @@
 
 #include "enet_crypto.h"
 #include "host_engine.hpp"
-
-namespace {
-
-void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw std::runtime_error(std::string("enet: ") + what + ": " + hipGetErrorString(e));
-}
-
-void enet_check(int rc, const char* what) {
-    if (rc != ENET_OK) throw std::runtime_error(std::string("enet: ") + what + ": " + enet_last_error());
-}
+#include "scalar.hpp"
 
 // ------------------------------------------------------------------------------ scalar routing
-namespace scalar {
+namespace enet::scalar {
 std::atomic<int> g_policy{ENET_SCALAR_AUTO};
 // ChaCha20 records from this size go to the MI355X under ENET_SCALAR_AUTO (INTEGRATION.md
 // measures the crossover: below it the host engine's AVX2 keystream beats PCIe + launch)
 std::atomic<uint64_t> g_crossover{256u << 10};
 std::atomic<int> g_on_error{0};
-std::atomic<uint64_t> g_host{0}, g_device{0}, g_failures{0}, g_launches{0}, g_records{0};
+std::atomic<uint64_t> g_failures{0}, g_launches{0}, g_records{0};
+// Per-call counters are sharded over cache lines: one shared atomic incremented by every session
+// thread on every 0.25 us HMAC capped 16 threads at 7 M calls/s (the reference does 11.6 M).
+struct alignas(64) CallShard {
+    std::atomic<uint64_t> host{0}, device{0};
+};
+CallShard g_shards[64];
+CallShard& shard() {
+    static std::atomic<unsigned> next{0};
+    thread_local CallShard& s = g_shards[next.fetch_add(1, std::memory_order_relaxed) & 63u];
+    return s;
+}
 std::atomic<uint32_t> g_inject{0};
 std::atomic<bool> g_reported{false};
 
@@ -72,8 +74,8 @@ bool device_for(uint64_t bytes, bool has_crossover) {
     return has_crossover && bytes >= g_crossover.load(std::memory_order_relaxed);
 }
 
-void host_call() { g_host.fetch_add(1, std::memory_order_relaxed); }
-void device_call() { g_device.fetch_add(1, std::memory_order_relaxed); }
+void host_call() { shard().host.fetch_add(1, std::memory_order_relaxed); }
+void device_call() { shard().device.fetch_add(1, std::memory_order_relaxed); }
 
 // throws like a failed HIP call when a test injected failures
 void maybe_inject() {
@@ -97,24 +99,19 @@ void device_failed(const char* what, const char* why) noexcept {
                      what, why);
 }
 
-// Run `dev` (device path); on any failure except bad_alloc, report and return false.
-template <class F>
-bool try_device(const char* what, F&& dev) {
-    try {
-        maybe_inject();
-        dev();
-        device_call();
-        return true;
-    } catch (const std::bad_alloc&) {
-        throw;
-    } catch (const std::exception& e) {
-        device_failed(what, e.what());
-    } catch (...) {
-        device_failed(what, "unknown error");
-    }
-    return false;
+}  // namespace enet::scalar
+
+namespace {
+namespace scalar = enet::scalar;
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("enet: ") + what + ": " + hipGetErrorString(e));
 }
-}  // namespace scalar
+
+void enet_check(int rc, const char* what) {
+    if (rc != ENET_OK) throw std::runtime_error(std::string("enet: ") + what + ": " + enet_last_error());
+}
+
 
 // Staging buffers + one stream per host thread, for the batch API and the scalar API's device
 // path under ENET_SCALAR_DEVICE.  Buffers of up to kZeroCopyMax bytes come from one pinned,
@@ -367,11 +364,13 @@ std::array<uint8_t, 32> device_hmac(std::span<const uint8_t> key, std::span<cons
 // ------------------------------------------------------------------------------ coalescer
 // ChaCha20::apply records routed to the MI355X.  Each caller queues its request; whichever caller
 // finds no launch in flight becomes the leader, takes EVERY pending request, and runs them as one
-// enet_chacha20_xor_batch (one H2D per record straight from the caller's span, one launch, one
-// D2H per record straight into the caller's vector); requests arriving meanwhile wait for the
-// next leader.  No artificial delay: a lone caller launches at once, and under load the batch
-// grows by itself while the previous one runs.  The leader's staging is process-wide (one launch
-// in flight), so session threads do not each pin device buffers.
+// enet_chacha20_xor_batch; requests arriving meanwhile wait for the next leader.  No artificial
+// delay: a lone caller launches at once, and under load the batch grows by itself while the
+// previous one runs.  The callers' vectors are pageable, and pageable hipMemcpy crawls on the
+// box (~0.8 GB/s round trip: a 64 KiB call took 167 us), so the leader copies
+// the records into a pinned, device-mapped arena and the kernel works on it in place over PCIe
+// (zero-copy: one launch, no DMA), then copies the results out.  One arena, grow-only up to
+// kArenaMax; records that do not fit are finished on the host engine.
 struct ChachaReq {
     const uint8_t* key;
     const uint8_t* nonce;
@@ -385,6 +384,7 @@ struct ChachaReq {
 
 class Coalescer {
 public:
+    static constexpr size_t kArenaMax = 256u << 20;
     static Coalescer& get() {
         static Coalescer* c = new Coalescer();  // never destroyed: no HIP calls during exit
         return *c;
@@ -401,23 +401,29 @@ public:
             std::vector<ChachaReq*> batch;
             batch.swap(pending_);
             lk.unlock();
-            bool ok = false;
-            try {
-                scalar::maybe_inject();
-                run(batch);
-                ok = true;
-            } catch (const std::exception& e) {
-                st_.reset();
-                scalar::device_failed("ChaCha20::apply", e.what());
-            } catch (...) {
-                st_.reset();
-                scalar::device_failed("ChaCha20::apply", "unknown error");
+            // groups that fit the arena; a record larger than the arena alone stays !ok (host)
+            size_t i = 0;
+            while (i < batch.size()) {
+                size_t j = i, bytes = 0;
+                while (j < batch.size() && (j == i || bytes + batch[j]->n <= kArenaMax)) bytes += batch[j++]->n;
+                std::vector<ChachaReq*> group(batch.begin() + (ptrdiff_t)i, batch.begin() + (ptrdiff_t)j);
+                bool ok = false;
+                if (bytes <= kArenaMax) {
+                    try {
+                        scalar::maybe_inject();
+                        run(group);
+                        ok = true;
+                    } catch (const std::exception& e) {
+                        scalar::device_failed("ChaCha20::apply", e.what());
+                    } catch (...) {
+                        scalar::device_failed("ChaCha20::apply", "unknown error");
+                    }
+                }
+                for (ChachaReq* q : group) q->ok = ok;
+                i = j;
             }
             lk.lock();
-            for (ChachaReq* q : batch) {
-                q->ok = ok;
-                q->done = true;
-            }
+            for (ChachaReq* q : batch) q->done = true;
             busy_ = false;
             cv_.notify_all();
         }
@@ -427,39 +433,56 @@ public:
 private:
     void run(const std::vector<ChachaReq*>& batch) {
         const size_t n = batch.size();
-        std::vector<uint64_t> off(n + 1, 0);
-        uint64_t mx = 0;
-        for (size_t i = 0; i < n; ++i) {
-            off[i + 1] = off[i] + batch[i]->n;
-            mx = std::max<uint64_t>(mx, batch[i]->n);
+        // arena: records back to back | offsets [n+1] | keys [n][32] | nonces [n][12] | counters [n]
+        uint64_t mx = 0, rec = 0;
+        for (const ChachaReq* q : batch) {
+            rec += q->n;
+            mx = std::max<uint64_t>(mx, q->n);
         }
-        std::vector<uint8_t> meta(48 * n);  // keys [n][32], nonces [n][12], counters [n]
-        for (size_t i = 0; i < n; ++i) {
-            std::memcpy(meta.data() + 32 * i, batch[i]->key, 32);
-            std::memcpy(meta.data() + 32 * n + 12 * i, batch[i]->nonce, 12);
-            std::memcpy(meta.data() + 44 * n + 4 * i, &batch[i]->counter, 4);
+        const size_t off_at = (rec + 255) & ~size_t(255), keys_at = off_at + 8 * (n + 1),
+                     non_at = keys_at + 32 * n, ctr_at = (non_at + 12 * n + 3) & ~size_t(3),
+                     total = ctr_at + 4 * n;
+        if (total > cap_) {
+            if (arena_) (void)hipHostFree(arena_);
+            arena_ = nullptr;
+            const size_t c = std::max(total, std::min(kArenaMax + (64u << 10), std::max<size_t>(2 * cap_, 4u << 20)));
+            cap_ = 0;
+            hip_check(hipHostMalloc(reinterpret_cast<void**>(&arena_), c, hipHostMallocMapped), "hipHostMalloc");
+            cap_ = c;
+            void* dp = nullptr;
+            hip_check(hipHostGetDevicePointer(&dp, arena_, 0), "hipHostGetDevicePointer");
+            dev_ = static_cast<uint8_t*>(dp);
         }
-        auto* arena = (uint8_t*)st_.get(S_IN, off[n]);
-        auto* doff = (uint64_t*)st_.get(S_INOFF, 8 * (n + 1));
-        auto* dmeta = (uint8_t*)st_.get(S_KEYS, meta.size());
-        for (size_t i = 0; i < n; ++i) st_.h2d(arena + off[i], batch[i]->in, batch[i]->n);
-        st_.h2d(doff, off.data(), 8 * (n + 1));
-        st_.h2d(dmeta, meta.data(), meta.size());
+        uint64_t* offs = reinterpret_cast<uint64_t*>(arena_ + off_at);
+        uint64_t o = 0;
+        for (size_t i = 0; i < n; ++i) {
+            offs[i] = o;
+            std::memcpy(arena_ + o, batch[i]->in, batch[i]->n);
+            o += batch[i]->n;
+            std::memcpy(arena_ + keys_at + 32 * i, batch[i]->key, 32);
+            std::memcpy(arena_ + non_at + 12 * i, batch[i]->nonce, 12);
+            std::memcpy(arena_ + ctr_at + 4 * i, &batch[i]->counter, 4);
+        }
+        offs[n] = o;
         enet_records r{};
         r.count = (uint32_t)n;
-        r.in_offsets = doff;
-        r.out_offsets = doff;
-        r.in = arena;
-        r.out = arena;  // in place
-        r.keys = dmeta;
+        r.in_offsets = reinterpret_cast<const uint64_t*>(dev_ + off_at);
+        r.out_offsets = r.in_offsets;
+        r.in = dev_;
+        r.out = dev_;  // in place
+        r.keys = dev_ + keys_at;
         r.key_stride = 32;
-        r.nonces = dmeta + 32 * n;
-        r.total_bytes_hint = off[n];
+        r.nonces = dev_ + non_at;
+        r.total_bytes_hint = rec;
         r.max_len_hint = (uint32_t)std::min<uint64_t>(mx, 0xffffffffu);
-        enet_check(enet_chacha20_xor_batch(&r, reinterpret_cast<const uint32_t*>(dmeta + 44 * n), st_.s()),
+        enet_check(enet_chacha20_xor_batch(&r, reinterpret_cast<const uint32_t*>(dev_ + ctr_at), st_.s()),
                    "chacha20 (coalesced)");
-        for (size_t i = 0; i < n; ++i) st_.d2h(batch[i]->out, arena + off[i], batch[i]->n);
-        st_.sync();
+        hip_check(hipStreamSynchronize(st_.s()), "hipStreamSynchronize");
+        o = 0;
+        for (size_t i = 0; i < n; ++i) {
+            std::memcpy(batch[i]->out, arena_ + o, batch[i]->n);
+            o += batch[i]->n;
+        }
         scalar::g_launches.fetch_add(1, std::memory_order_relaxed);
         scalar::g_records.fetch_add(n, std::memory_order_relaxed);
     }
@@ -468,6 +491,9 @@ private:
     std::condition_variable cv_;
     std::vector<ChachaReq*> pending_;
     bool busy_ = false;
+    uint8_t* arena_ = nullptr;  // pinned, device-mapped
+    uint8_t* dev_ = nullptr;    // its device address
+    size_t cap_ = 0;
     Staging st_;
 };
 
@@ -494,16 +520,22 @@ int enet_scalar_set_on_device_error(int mode) {
 
 void enet_scalar_get_stats(enet_scalar_stats* out) {
     if (!out) return;
-    out->host_calls = scalar::g_host.load();
-    out->device_calls = scalar::g_device.load();
+    out->host_calls = 0;
+    out->device_calls = 0;
+    for (const auto& sh : scalar::g_shards) {
+        out->host_calls += sh.host.load();
+        out->device_calls += sh.device.load();
+    }
     out->device_failures = scalar::g_failures.load();
     out->coalesced_launches = scalar::g_launches.load();
     out->coalesced_records = scalar::g_records.load();
 }
 
 void enet_scalar_reset_stats(void) {
-    scalar::g_host = 0;
-    scalar::g_device = 0;
+    for (auto& sh : scalar::g_shards) {
+        sh.host = 0;
+        sh.device = 0;
+    }
     scalar::g_failures = 0;
     scalar::g_launches = 0;
     scalar::g_records = 0;
@@ -923,26 +955,6 @@ std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std:
     enet_check(enet_wire_open_batch(&d.r, macs, dok, st.s()), "wire_open");
     st.d2h(ok.data(), dok, n);
     return download(st, d, out_off);
-}
-
-bool FrameQueue::push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message) {
-    if (message.size() + 32 > kMaxPayloadSize) return false;
-    Nonce nonce{};
-    std::random_device rd;
-    for (auto& byte : nonce.bytes) byte = static_cast<std::uint8_t>(rd());
-    keys_.push_back(session_key);
-    nonces_.push_back(nonce);
-    messages_.emplace_back(message.begin(), message.end());
-    return true;
-}
-
-std::vector<std::vector<std::uint8_t>> FrameQueue::flush() {
-    std::vector<std::span<const std::uint8_t>> views(messages_.begin(), messages_.end());
-    auto frames = wire_seal(keys_, nonces_, views);
-    keys_.clear();
-    nonces_.clear();
-    messages_.clear();
-    return frames;
 }
 
 // ------------------------------------------------------------------------------ proof of work

@@ -1,0 +1,305 @@
+// frame_queue.cpp -- the cross-session frame queues of Batch.hpp.
+//
+// Many session threads each submit one frame and block.  Whichever waiting thread finds no flush
+// in flight becomes the leader: it keeps collecting until the queue holds max_frames frames or
+// max_bytes bytes or max_delay has passed, takes what is queued (up to the limits), runs ONE
+// batched pass -- crypto::batch::wire_seal / wire_open on the MI355X -- writes every caller's
+// result into that caller's request and wakes them all.  A request is owned by the thread that
+// submitted it (it lives on that thread's stack until `done`), results are matched by request,
+// never by position in some shared buffer, so sessions cannot see each other's frames.
+//
+// Reference: SessionManager::send (src/network/SessionManager.cpp:337-388), receive_loop
+// (:703-854) and protocol::encode_signed / decode_signed (src/protocol/Message.cpp:305-328).
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <vector>
+
+#include "enet_crypto.h"
+#include "ephemeralnet/crypto/Batch.hpp"
+#include "host_engine.hpp"
+#include "scalar.hpp"
+
+namespace ephemeralnet::crypto::batch {
+
+namespace {
+
+constexpr std::size_t kHeader = 16;  // nonce(12) || BE32(|body|), SessionManager.cpp:376-385
+constexpr std::size_t kMac = 32;
+
+struct Req {
+    const std::uint8_t* key;
+    std::span<const std::uint8_t> in;  // message (send) or whole frame (receive)
+    std::vector<std::uint8_t> out;     // frame (send) or message (receive)
+    bool ok = false;
+    bool done = false;
+};
+
+// The leader protocol shared by both directions; Exec(std::vector<Req*>&) fills out / ok.
+class Flusher {
+public:
+    explicit Flusher(const FrameQueueOptions& o) : opt_(o) {
+        opt_.max_frames = std::max<std::size_t>(1, opt_.max_frames);
+    }
+
+    template <class Exec>
+    void submit(Req& r, Exec&& exec) {
+        std::unique_lock<std::mutex> lk(mu_);
+        pending_.push_back(&r);
+        bytes_ += r.in.size();
+        if (full()) more_.notify_one();
+        while (!r.done) {
+            if (busy_) {
+                done_.wait(lk);
+                continue;
+            }
+            busy_ = true;
+            // collect until a size trigger or the deadline
+            const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
+            while (!full() && more_.wait_until(lk, deadline) != std::cv_status::timeout) {
+            }
+            std::vector<Req*> batch;
+            std::size_t take = 0, b = 0;
+            while (take < pending_.size() && take < opt_.max_frames &&
+                   (take == 0 || b + pending_[take]->in.size() <= opt_.max_bytes)) {
+                b += pending_[take]->in.size();
+                ++take;
+            }
+            batch.assign(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
+            pending_.erase(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
+            bytes_ -= b;
+            lk.unlock();
+            bool host = false;
+            try {
+                host = exec(batch);
+            } catch (...) {  // only std::bad_alloc gets here: fail the batch, keep the queue alive
+                lk.lock();
+                for (Req* q : batch) {
+                    q->ok = false;
+                    q->done = true;
+                }
+                busy_ = false;
+                done_.notify_all();
+                throw;
+            }
+            lk.lock();
+            for (Req* q : batch) q->done = true;
+            stats_.frames += batch.size();
+            stats_.flushes += 1;
+            stats_.host_flushes += host ? 1 : 0;
+            busy_ = false;
+            done_.notify_all();
+        }
+    }
+
+    FrameQueueStats stats() {
+        std::lock_guard<std::mutex> lk(mu_);
+        return stats_;
+    }
+
+private:
+    bool full() const { return pending_.size() >= opt_.max_frames || bytes_ >= opt_.max_bytes; }
+
+    FrameQueueOptions opt_;
+    std::mutex mu_;
+    std::condition_variable more_, done_;
+    std::vector<Req*> pending_;
+    std::size_t bytes_ = 0;
+    bool busy_ = false;
+    FrameQueueStats stats_{};
+};
+
+void put_be32(std::uint8_t* p, std::uint32_t v) {
+    p[0] = (std::uint8_t)(v >> 24);
+    p[1] = (std::uint8_t)(v >> 16);
+    p[2] = (std::uint8_t)(v >> 8);
+    p[3] = (std::uint8_t)v;
+}
+
+// host engine: SessionManager::send for one frame
+std::vector<std::uint8_t> host_wire_seal(const std::uint8_t key[32], const std::uint8_t nonce[12],
+                                         std::span<const std::uint8_t> m) {
+    std::vector<std::uint8_t> f(kHeader + m.size() + kMac);
+    std::memcpy(f.data(), nonce, 12);
+    put_be32(f.data() + 12, (std::uint32_t)(m.size() + kMac));
+    if (!m.empty()) std::memcpy(f.data() + kHeader, m.data(), m.size());
+    const auto mac = enet::host::hmac_sha256(key, 32, m.data(), m.size());
+    std::memcpy(f.data() + kHeader + m.size(), mac.data(), kMac);
+    enet::host::chacha20_xor(key, nonce, 0, f.data() + kHeader, f.data() + kHeader, m.size() + kMac);
+    return f;
+}
+
+// the length checks of receive_loop (:760-796) and decode_signed (Message.cpp:315)
+bool frame_shape_ok(std::span<const std::uint8_t> f) {
+    if (f.size() < kHeader + kMac) return false;
+    const std::uint32_t len = (std::uint32_t)f[12] << 24 | (std::uint32_t)f[13] << 16 |
+                              (std::uint32_t)f[14] << 8 | f[15];
+    return (std::uint64_t)len == f.size() - kHeader && len <= FrameQueue::kMaxPayloadSize;
+}
+
+// host engine: receive_loop decrypt + decode_signed verify for one frame (shape already checked)
+bool host_wire_open(const std::uint8_t key[32], std::span<const std::uint8_t> f, std::vector<std::uint8_t>& m) {
+    const std::size_t body = f.size() - kHeader;
+    std::vector<std::uint8_t> pt(body);
+    enet::host::chacha20_xor(key, f.data(), 0, f.data() + kHeader, pt.data(), body);
+    const std::size_t ml = body - kMac;
+    const auto mac = enet::host::hmac_sha256(key, 32, pt.data(), ml);
+    std::uint8_t diff = 0;
+    for (std::size_t i = 0; i < kMac; ++i) diff |= (std::uint8_t)(mac[i] ^ pt[ml + i]);
+    if (diff) return false;
+    pt.resize(ml);
+    m = std::move(pt);
+    return true;
+}
+
+void draw_nonces(std::random_device& rd, std::vector<Nonce>& nonces) {
+    for (auto& n : nonces)
+        for (int i = 0; i < 12; i += 4) {
+            const std::uint32_t v = rd();
+            std::memcpy(n.bytes.data() + i, &v, 4);
+        }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ send
+struct FrameQueue::Impl {
+    explicit Impl(const FrameQueueOptions& o) : flusher(o) {}
+    Flusher flusher;
+    std::mutex rd_mu;
+    std::random_device rd;
+    // push / flush
+    mutable std::mutex manual_mu;
+    std::vector<std::array<std::uint8_t, 32>> keys;
+    std::vector<std::vector<std::uint8_t>> messages;
+
+    // seal `batch` (message spans + keys); returns true when the host engine served it
+    bool seal(std::vector<Req*>& batch) {
+        const std::size_t n = batch.size();
+        std::vector<Nonce> nonces(n);
+        {
+            std::lock_guard<std::mutex> lk(rd_mu);
+            draw_nonces(rd, nonces);
+        }
+        if (enet::scalar::g_policy.load() != ENET_SCALAR_HOST) {
+            std::vector<std::array<std::uint8_t, 32>> ks(n);
+            std::vector<std::span<const std::uint8_t>> ms(n);
+            for (std::size_t i = 0; i < n; ++i) {
+                std::memcpy(ks[i].data(), batch[i]->key, 32);
+                ms[i] = batch[i]->in;
+            }
+            std::vector<std::vector<std::uint8_t>> frames;
+            if (enet::scalar::try_device("FrameQueue flush", [&] { frames = wire_seal(ks, nonces, ms); })) {
+                for (std::size_t i = 0; i < n; ++i) {
+                    batch[i]->out = std::move(frames[i]);
+                    batch[i]->ok = true;
+                }
+                return false;
+            }
+        }
+        enet::scalar::host_call();
+        for (std::size_t i = 0; i < n; ++i) {
+            batch[i]->out = host_wire_seal(batch[i]->key, nonces[i].bytes.data(), batch[i]->in);
+            batch[i]->ok = true;
+        }
+        return true;
+    }
+};
+
+FrameQueue::FrameQueue() : FrameQueue(FrameQueueOptions{}) {}
+FrameQueue::FrameQueue(FrameQueueOptions options) : impl_(new Impl(options)) {}
+FrameQueue::~FrameQueue() { delete impl_; }
+
+std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::uint8_t, 32>& session_key,
+                                                          std::span<const std::uint8_t> message) {
+    if (message.size() + kMac > kMaxPayloadSize) return std::nullopt;  // SessionManager.cpp:358-360
+    Req r{session_key.data(), message, {}};
+    impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->seal(b); });
+    if (!r.ok) return std::nullopt;
+    return std::move(r.out);
+}
+
+bool FrameQueue::push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message) {
+    if (message.size() + kMac > kMaxPayloadSize) return false;
+    std::lock_guard<std::mutex> lk(impl_->manual_mu);
+    impl_->keys.push_back(session_key);
+    impl_->messages.emplace_back(message.begin(), message.end());
+    return true;
+}
+
+std::size_t FrameQueue::size() const {
+    std::lock_guard<std::mutex> lk(impl_->manual_mu);
+    return impl_->messages.size();
+}
+
+std::vector<std::vector<std::uint8_t>> FrameQueue::flush() {
+    std::vector<std::array<std::uint8_t, 32>> keys;
+    std::vector<std::vector<std::uint8_t>> messages;
+    {
+        std::lock_guard<std::mutex> lk(impl_->manual_mu);
+        keys.swap(impl_->keys);
+        messages.swap(impl_->messages);
+    }
+    std::vector<Req> reqs(messages.size());
+    std::vector<Req*> batch(messages.size());
+    for (std::size_t i = 0; i < messages.size(); ++i) {
+        reqs[i].key = keys[i].data();
+        reqs[i].in = messages[i];
+        batch[i] = &reqs[i];
+    }
+    std::vector<std::vector<std::uint8_t>> frames(messages.size());
+    if (!batch.empty()) impl_->seal(batch);
+    for (std::size_t i = 0; i < frames.size(); ++i) frames[i] = std::move(reqs[i].out);
+    return frames;
+}
+
+FrameQueueStats FrameQueue::stats() const { return impl_->flusher.stats(); }
+
+// ------------------------------------------------------------------------------ receive
+struct FrameReceiveQueue::Impl {
+    explicit Impl(const FrameQueueOptions& o) : flusher(o) {}
+    Flusher flusher;
+
+    bool open(std::vector<Req*>& batch) {
+        const std::size_t n = batch.size();
+        if (enet::scalar::g_policy.load() != ENET_SCALAR_HOST) {
+            std::vector<std::array<std::uint8_t, 32>> ks(n);
+            std::vector<std::span<const std::uint8_t>> fs(n);
+            for (std::size_t i = 0; i < n; ++i) {
+                std::memcpy(ks[i].data(), batch[i]->key, 32);
+                fs[i] = batch[i]->in;
+            }
+            std::vector<std::vector<std::uint8_t>> msgs;
+            std::vector<std::uint8_t> ok;
+            if (enet::scalar::try_device("FrameReceiveQueue flush", [&] { msgs = wire_open(ks, fs, ok); })) {
+                for (std::size_t i = 0; i < n; ++i) {
+                    batch[i]->ok = ok[i] == 1;
+                    if (batch[i]->ok) batch[i]->out = std::move(msgs[i]);
+                }
+                return false;
+            }
+        }
+        enet::scalar::host_call();
+        for (std::size_t i = 0; i < n; ++i) batch[i]->ok = host_wire_open(batch[i]->key, batch[i]->in, batch[i]->out);
+        return true;
+    }
+};
+
+FrameReceiveQueue::FrameReceiveQueue() : FrameReceiveQueue(FrameQueueOptions{}) {}
+FrameReceiveQueue::FrameReceiveQueue(FrameQueueOptions options) : impl_(new Impl(options)) {}
+FrameReceiveQueue::~FrameReceiveQueue() { delete impl_; }
+
+std::optional<std::vector<std::uint8_t>> FrameReceiveQueue::open(const std::array<std::uint8_t, 32>& session_key,
+                                                                 std::span<const std::uint8_t> frame) {
+    if (!frame_shape_ok(frame)) return std::nullopt;  // never reaches a flush
+    Req r{session_key.data(), frame, {}};
+    impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->open(b); });
+    if (!r.ok) return std::nullopt;
+    return std::move(r.out);
+}
+
+FrameQueueStats FrameReceiveQueue::stats() const { return impl_->flusher.stats(); }
+
+}  // namespace ephemeralnet::crypto::batch

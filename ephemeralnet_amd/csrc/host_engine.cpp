@@ -1,8 +1,9 @@
 // host_engine.cpp -- scalar SHA-256 / HMAC-SHA256 / ChaCha20 on the calling CPU thread
 // (host_engine.hpp says why).  x86-64: SHA-256 on the SHA extensions (sha256rnds2 / msg1 /
-// msg2), ChaCha20 eight blocks at a time in AVX2 registers (one 32-bit state word of eight
-// blocks per ymm register, counters base + 0..7 wrapping mod 2^32 like ChaCha20.cpp:110), both
-// picked at run time from cpuid; portable C++ otherwise and for the tails.
+// msg2); ChaCha20 sixteen blocks at a time in AVX-512 registers (one 32-bit state word of 16
+// blocks per zmm register, vprold rotates, counters base + 0..15 wrapping mod 2^32 like
+// ChaCha20.cpp:110), eight at a time in AVX2 for a 512-byte remainder; all picked at run time
+// from cpuid; portable C++ otherwise and for the tails.
 #include "host_engine.hpp"
 
 #include <atomic>
@@ -229,7 +230,75 @@ __attribute__((target("avx2"))) void chacha_avx2(std::uint32_t s[16], const std:
 #undef ENET_VROT
     _mm256_zeroupper();
 }
+// Sixteen blocks per step in zmm registers, counters s[12] + 0..15; n16 = whole 1 KiB steps.
+// AVX-512 has the 32-bit rotate (vprold): one instruction per rotation instead of three.
+__attribute__((target("avx512f"))) void chacha_avx512(std::uint32_t s[16], const std::uint8_t* in,
+                                                    std::uint8_t* out, std::size_t n16) {
+    const __m512i lanes = _mm512_set_epi32(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
+    __m512i init[16];
+    for (int i = 0; i < 16; ++i) init[i] = _mm512_set1_epi32((int)s[i]);
+#define ENET_ZQR(a, b, c, d)                                                                  \
+    a = _mm512_add_epi32(a, b); d = _mm512_rol_epi32(_mm512_xor_si512(d, a), 16);            \
+    c = _mm512_add_epi32(c, d); b = _mm512_rol_epi32(_mm512_xor_si512(b, c), 12);            \
+    a = _mm512_add_epi32(a, b); d = _mm512_rol_epi32(_mm512_xor_si512(d, a), 8);             \
+    c = _mm512_add_epi32(c, d); b = _mm512_rol_epi32(_mm512_xor_si512(b, c), 7)
+    for (; n16; --n16, in += 1024, out += 1024) {
+        init[12] = _mm512_add_epi32(_mm512_set1_epi32((int)s[12]), lanes);  // u32 wrap per lane
+        __m512i x[16];
+        for (int i = 0; i < 16; ++i) x[i] = init[i];
+        for (int r = 0; r < 10; ++r) {
+            ENET_ZQR(x[0], x[4], x[8], x[12]);
+            ENET_ZQR(x[1], x[5], x[9], x[13]);
+            ENET_ZQR(x[2], x[6], x[10], x[14]);
+            ENET_ZQR(x[3], x[7], x[11], x[15]);
+            ENET_ZQR(x[0], x[5], x[10], x[15]);
+            ENET_ZQR(x[1], x[6], x[11], x[12]);
+            ENET_ZQR(x[2], x[7], x[8], x[13]);
+            ENET_ZQR(x[3], x[4], x[9], x[14]);
+        }
+        for (int i = 0; i < 16; ++i) x[i] = _mm512_add_epi32(x[i], init[i]);
+        // 16x16 transpose (word x block -> block x word): after the 32- and 64-bit unpacks,
+        // u[4k + e] holds words 4k..4k+3 of block 4L + e in its 128-bit lane L; the two
+        // shuffle_i32x4 rounds gather a block's four lanes
+        __m512i t[16], u[16];
+        for (int k = 0; k < 8; ++k) {
+            t[2 * k] = _mm512_unpacklo_epi32(x[2 * k], x[2 * k + 1]);
+            t[2 * k + 1] = _mm512_unpackhi_epi32(x[2 * k], x[2 * k + 1]);
+        }
+        for (int k = 0; k < 4; ++k) {
+            u[4 * k + 0] = _mm512_unpacklo_epi64(t[4 * k], t[4 * k + 2]);
+            u[4 * k + 1] = _mm512_unpackhi_epi64(t[4 * k], t[4 * k + 2]);
+            u[4 * k + 2] = _mm512_unpacklo_epi64(t[4 * k + 1], t[4 * k + 3]);
+            u[4 * k + 3] = _mm512_unpackhi_epi64(t[4 * k + 1], t[4 * k + 3]);
+        }
+        for (int e = 0; e < 4; ++e) {
+            const __m512i w0 = _mm512_shuffle_i32x4(u[e], u[4 + e], 0x44);
+            const __m512i w1 = _mm512_shuffle_i32x4(u[e], u[4 + e], 0xEE);
+            const __m512i w2 = _mm512_shuffle_i32x4(u[8 + e], u[12 + e], 0x44);
+            const __m512i w3 = _mm512_shuffle_i32x4(u[8 + e], u[12 + e], 0xEE);
+            const __m512i blk[4] = {_mm512_shuffle_i32x4(w0, w2, 0x88), _mm512_shuffle_i32x4(w0, w2, 0xDD),
+                                    _mm512_shuffle_i32x4(w1, w3, 0x88), _mm512_shuffle_i32x4(w1, w3, 0xDD)};
+            for (int L = 0; L < 4; ++L) {
+                const std::size_t o = 64 * (std::size_t)(4 * L + e);
+                const __m512i v = _mm512_loadu_si512(in + o);
+                _mm512_storeu_si512(out + o, _mm512_xor_si512(v, blk[L]));
+            }
+        }
+        s[12] += 16u;
+    }
+#undef ENET_ZQR
+    _mm256_zeroupper();
+}
 #endif
+
+bool have_avx512() {
+#if defined(__x86_64__)
+    static const bool v = __builtin_cpu_supports("avx512f");
+    return v;
+#else
+    return false;
+#endif
+}
 
 }  // namespace
 
@@ -237,8 +306,8 @@ void force_portable(bool on) { g_portable.store(on, std::memory_order_relaxed); 
 
 const char* isa() {
     if (g_portable.load(std::memory_order_relaxed)) return "portable";
-    const bool s = have_shani(), a = have_avx2();
-    return s && a ? "sha-ni+avx2" : s ? "sha-ni" : a ? "avx2" : "portable";
+    const bool s = have_shani(), a = have_avx2(), z = have_avx512();
+    return s && z ? "sha-ni+avx512" : s && a ? "sha-ni+avx2" : s ? "sha-ni" : z ? "avx512" : a ? "avx2" : "portable";
 }
 
 void sha256_blocks(std::uint32_t state[8], const std::uint8_t* p, std::size_t blocks) {
@@ -345,6 +414,13 @@ void chacha20_xor(const std::uint8_t key[32], const std::uint8_t nonce[12], std:
     s[12] = counter;
     for (int i = 0; i < 3; ++i) s[13 + i] = le32(nonce + 4 * i);
 #if defined(__x86_64__)
+    if (have_avx512() && !g_portable.load(std::memory_order_relaxed) && n >= 1024) {
+        const std::size_t n16 = n / 1024;
+        chacha_avx512(s, in, out, n16);
+        in += 1024 * n16;
+        out += 1024 * n16;
+        n -= 1024 * n16;
+    }
     if (have_avx2() && !g_portable.load(std::memory_order_relaxed) && n >= 512) {
         const std::size_t n8 = n / 512;
         chacha_avx2(s, in, out, n8);

@@ -5,7 +5,9 @@
 #pragma once
 
 #include <array>
+#include <chrono>
 #include <cstdint>
+#include <optional>
 #include <span>
 #include <string_view>
 #include <vector>
@@ -76,23 +78,76 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open(
     std::span<const std::array<std::uint8_t, 32>> session_keys,
     std::span<const std::span<const std::uint8_t>> frames, std::vector<std::uint8_t>& ok);
 
-// Send-side batching queue across sessions: callers push (session key,
-// encoded message) pairs from any session and one flush() seals them all in a single device
-// pass.  Nonces are drawn from std::random_device as in SessionManager::send (:366-372).
+// Cross-session frame queues.  SessionManager runs one detached reader
+// thread per session (SessionManager.cpp:332-333, receive_loop :703-854) and sends from whatever
+// thread calls Node::send_secure (:337-388).  Instead of one ChaCha20 + HMAC per frame on each of
+// those threads, every thread hands its frame to a shared queue and blocks; the queue flushes
+// when it holds max_frames frames or max_bytes bytes, or max_delay after the first waiting frame,
+// and ONE batched pass (crypto::batch::wire_seal / wire_open on the MI355X) serves everything
+// queued, each caller getting back exactly its own result.  Thread-safe; results are bit-exact
+// with the per-frame reference path.  Routing follows enet_scalar_set_policy: ENET_SCALAR_HOST
+// serves a flush on the host engine, and a failed device flush is finished on the host engine
+// (never an exception into a session thread).
+struct FrameQueueOptions {
+    std::size_t max_frames = 4096;                     // flush at this many queued frames
+    std::size_t max_bytes = 8u << 20;                  // ... or this many queued bytes
+    std::chrono::microseconds max_delay{100};          // ... or this long after a flush could start
+};
+struct FrameQueueStats {
+    std::uint64_t frames = 0;   // frames served
+    std::uint64_t flushes = 0;  // batched passes (frames / flushes = mean batch)
+    std::uint64_t host_flushes = 0;  // passes served by the host engine (policy or device failure)
+};
+
+// Send side: nonce(12) || BE32(|body|) || ChaCha20_{K,nonce,0}(m || HMAC_K(m)), the frame
+// SessionManager::send writes (SessionManager.cpp:362-387).  Nonces: 12 bytes per frame from
+// std::random_device, as SessionManager.cpp:365-371 draws them, taken once per flush.
 class ENET_CXX_API FrameQueue {
 public:
     static constexpr std::size_t kMaxPayloadSize = 1024 * 1024;  // SessionManager.cpp:87
-    // false when the signed payload (message + 32-byte MAC) exceeds kMaxPayloadSize, as
-    // SessionManager::send returns false (:358-360); nothing is queued then.
+    FrameQueue();
+    explicit FrameQueue(FrameQueueOptions options);
+    ~FrameQueue();
+    FrameQueue(const FrameQueue&) = delete;
+    FrameQueue& operator=(const FrameQueue&) = delete;
+
+    // Seal one message for one session; blocks until the flush carrying it has run.  nullopt
+    // when the signed payload (message + 32-byte MAC) exceeds kMaxPayloadSize, as
+    // SessionManager::send returns false (:358-360).
+    std::optional<std::vector<std::uint8_t>> seal(const std::array<std::uint8_t, 32>& session_key,
+                                                  std::span<const std::uint8_t> message);
+    // Explicit batching (a sender that collects frames itself): push queues a message (false =
+    // too large, nothing queued), flush() seals every pushed message in one pass and returns the
+    // wire frames in push order.  Thread-safe; independent of seal()'s queue.
     bool push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message);
-    std::size_t size() const { return messages_.size(); }
-    // wire frames in push order; empties the queue
+    std::size_t size() const;
     std::vector<std::vector<std::uint8_t>> flush();
+    FrameQueueStats stats() const;
 
 private:
-    std::vector<std::array<std::uint8_t, 32>> keys_;
-    std::vector<Nonce> nonces_;
-    std::vector<std::vector<std::uint8_t>> messages_;
+    struct Impl;
+    Impl* impl_;
+};
+
+// Receive side: the inverse for frames read off any session's socket (receive_loop :744-822 +
+// decode_signed, Message.cpp:313-328): nullopt when the frame is shorter than its header, its
+// BE32 length disagrees with the body or exceeds kMaxPayloadSize, the body is shorter than the
+// MAC, or the HMAC does not verify; otherwise the message (the body minus its 32-byte MAC).
+class ENET_CXX_API FrameReceiveQueue {
+public:
+    FrameReceiveQueue();
+    explicit FrameReceiveQueue(FrameQueueOptions options);
+    ~FrameReceiveQueue();
+    FrameReceiveQueue(const FrameReceiveQueue&) = delete;
+    FrameReceiveQueue& operator=(const FrameReceiveQueue&) = delete;
+
+    std::optional<std::vector<std::uint8_t>> open(const std::array<std::uint8_t, 32>& session_key,
+                                                  std::span<const std::uint8_t> frame);
+    FrameQueueStats stats() const;
+
+private:
+    struct Impl;
+    Impl* impl_;
 };
 
 // Proof of work.  Every PoW in the reference hashes

@@ -1,0 +1,138 @@
+// queue_stress.cpp -- many session threads through the cross-session frame queues at once
+// (crypto::batch::FrameQueue / FrameReceiveQueue).
+//
+// usage: queue_stress <policy auto|device|host> <threads> <frames per thread> <seed>
+// Phase 1: every thread seals its own session's messages (lengths 0..3000, some 64 KiB, one
+// frame of the 1 MiB maximum payload per run) through ONE shared FrameQueue.  Phase 2: every
+// thread opens its own frames through ONE shared FrameReceiveQueue, with every 7th frame
+// tampered (nonce, length field, body or MAC byte) and every 11th opened under the NEXT thread's
+// session key.  Each thread checks that exactly the untouched frames come back, byte-equal to its
+// own messages.  Prints a sample of (key, message, frame) lines for the oracle check in
+// tests/test_frame_queue.py and a summary line.
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "enet_crypto.h"
+#include "ephemeralnet/crypto/Batch.hpp"
+
+using namespace ephemeralnet::crypto;
+using namespace ephemeralnet::crypto::batch;
+
+namespace {
+
+std::uint64_t splitmix(std::uint64_t& s) {
+    std::uint64_t z = (s += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+std::string hex(const std::vector<std::uint8_t>& v) {
+    static const char* d = "0123456789abcdef";
+    std::string s;
+    for (auto b : v) {
+        s += d[b >> 4];
+        s += d[b & 15];
+    }
+    return s.empty() ? "-" : s;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const std::string policy = argc > 1 ? argv[1] : "auto";
+    const int T = argc > 2 ? std::atoi(argv[2]) : 16;
+    const int F = argc > 3 ? std::atoi(argv[3]) : 200;
+    const std::uint64_t seed = argc > 4 ? std::strtoull(argv[4], nullptr, 10) : 1;
+    enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
+                                                                                      : ENET_SCALAR_AUTO, 0);
+    std::vector<std::array<std::uint8_t, 32>> keys(T);
+    std::vector<std::vector<std::vector<std::uint8_t>>> msgs(T), frames(T);
+    for (int t = 0; t < T; ++t) {
+        std::uint64_t s = seed * 1000003u + (std::uint64_t)t;
+        for (auto& b : keys[t]) b = (std::uint8_t)splitmix(s);
+        msgs[t].resize(F);
+        for (int i = 0; i < F; ++i) {
+            std::size_t L = splitmix(s) % 3001;
+            if (i % 53 == 5) L = 65536;
+            if (t == 0 && i == 1) L = FrameQueue::kMaxPayloadSize - 32;  // largest signed payload
+            msgs[t][i].resize(L);
+            for (auto& b : msgs[t][i]) b = (std::uint8_t)splitmix(s);
+        }
+    }
+    FrameQueueOptions opt;
+    opt.max_frames = 512;
+    opt.max_delay = std::chrono::microseconds(200);
+    FrameQueue tx(opt);
+    FrameReceiveQueue rx(opt);
+    std::atomic<int> bad{0}, oversize_ok{0};
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                frames[t].resize(F);
+                for (int i = 0; i < F; ++i) {
+                    auto f = tx.seal(keys[t], msgs[t][i]);
+                    if (!f || f->size() != msgs[t][i].size() + 48) {
+                        ++bad;
+                        continue;
+                    }
+                    frames[t][i] = std::move(*f);
+                }
+                // too large: refused like SessionManager::send, nothing queued
+                std::vector<std::uint8_t> huge(FrameQueue::kMaxPayloadSize - 31);
+                if (!tx.seal(keys[t], huge)) ++oversize_ok;
+            });
+        for (auto& x : th) x.join();
+    }
+    std::atomic<int> opened{0}, rejected{0}, wrong{0};
+    {
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                for (int i = 0; i < F; ++i) {
+                    std::vector<std::uint8_t> f = frames[t][i];
+                    if (f.empty()) continue;
+                    bool expect_ok = true;
+                    auto key = keys[t];
+                    if (i % 7 == 3) {  // tamper: nonce, length field, body or MAC byte
+                        const std::size_t pos[4] = {5, 13, 16 + msgs[t][i].size() / 2, f.size() - 1};
+                        f[pos[(i / 7) % 4]] ^= 0x10;
+                        expect_ok = false;
+                    } else if (i % 11 == 4) {  // another session's key
+                        key = keys[(t + 1) % T];
+                        expect_ok = T == 1;
+                    }
+                    auto m = rx.open(key, f);
+                    if (m) ++opened;
+                    else ++rejected;
+                    if ((bool)m != expect_ok || (m && *m != msgs[t][i])) ++wrong;
+                }
+            });
+        for (auto& x : th) x.join();
+    }
+    // sample for the oracle: the first 3 frames of every thread with a message <= 4 KiB
+    for (int t = 0; t < T; ++t) {
+        int shown = 0;
+        for (int i = 0; i < F && shown < 3; ++i) {
+            if (msgs[t][i].size() > 4096 || frames[t][i].empty()) continue;
+            std::printf("frame %s %s %s\n", hex(std::vector<std::uint8_t>(keys[t].begin(), keys[t].end())).c_str(),
+                        hex(msgs[t][i]).c_str(), hex(frames[t][i]).c_str());
+            ++shown;
+        }
+    }
+    const auto st = tx.stats(), sr = rx.stats();
+    enet_scalar_stats ss{};
+    enet_scalar_get_stats(&ss);
+    std::printf("summary bad=%d oversize_refused=%d opened=%d rejected=%d wrong=%d tx_frames=%llu tx_flushes=%llu "
+                "tx_host_flushes=%llu rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu device_failures=%llu\n",
+                bad.load(), oversize_ok.load(), opened.load(), rejected.load(), wrong.load(),
+                (unsigned long long)st.frames, (unsigned long long)st.flushes, (unsigned long long)st.host_flushes,
+                (unsigned long long)sr.frames, (unsigned long long)sr.flushes, (unsigned long long)sr.host_flushes,
+                (unsigned long long)ss.device_failures);
+    return (bad || wrong || oversize_ok != T) ? 1 : 0;
+}

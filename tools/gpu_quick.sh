@@ -20,6 +20,11 @@ for args in "--records 1048576 --record-bytes 1500" "--mode wire --records 10485
   step "  $args"
   timeout -k 10 240 python bench.py --steps 10 --warmup 3 --no-cpu-baseline $args >> $O/side.jsonl 2>> $O/side.err
 done
+step scalar latency
+for pol in auto device; do
+  timeout -k 10 180 oracle/_ref/scalar_latency_gpu 200 $pol 16 > $O/latency_$pol.jsonl 2> $O/latency_$pol.err
+done
+timeout -k 10 180 oracle/_ref/scalar_latency_ref 200 x 16 > $O/latency_ref.jsonl 2> $O/latency_ref.err
 if [ "${2:-}" = pmc ]; then
 step pmc
 timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --no-power --steps 3 --warmup 1 > $O/pmc.log 2>&1

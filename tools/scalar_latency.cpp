@@ -10,12 +10,18 @@
 // 64 KiB chunk, and the Node.cpp:269-292 handshake PoW written as the reference writes it (one
 // Sha256 per attempt).  With ENET_BATCH the drop-in crypto::batch::compute_handshake_pow (one device
 // search) is timed beside it.  Output: one JSON line per case, median and mean microseconds.
+//
+// usage: scalar_latency [reps] [policy auto|device|host (drop-in build only)] [threads]
+// After the single-thread latencies, `threads` threads call the same API concurrently for ~1 s
+// per case (the reference's per-session reader threads, SessionManager.cpp:332,703) and the
+// aggregate calls/s and GB/s are printed ("mt_*" cases).
 #include "ephemeralnet/crypto/ChaCha20.hpp"
 #include "ephemeralnet/crypto/CryptoManager.hpp"
 #include "ephemeralnet/crypto/HmacSha256.hpp"
 #include "ephemeralnet/crypto/Sha256.hpp"
 #ifdef ENET_BATCH
 #include "ephemeralnet/crypto/Batch.hpp"
+#include "enet_crypto.h"
 #endif
 
 #include <algorithm>
@@ -25,7 +31,9 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -47,6 +55,37 @@ void run(const char* name, std::size_t bytes, int reps, const std::function<void
     std::printf("{\"case\": \"%s\", \"bytes\": %zu, \"reps\": %d, \"median_us\": %.2f, \"mean_us\": %.2f, "
                 "\"p10_us\": %.2f, \"p90_us\": %.2f}\n",
                 name, bytes, reps, us[reps / 2], sum / reps, us[reps / 10], us[(reps * 9) / 10]);
+    std::fflush(stdout);
+}
+
+// `threads` threads call f(thread) back to back for ~secs; aggregate rate
+void run_mt(const char* name, std::size_t bytes, int threads, double secs,
+            const std::function<void(int, std::vector<std::uint8_t>&)>& f) {
+    std::atomic<bool> go{false}, stop{false};
+    std::vector<std::uint64_t> calls(threads, 0);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t)
+        ts.emplace_back([&, t] {
+            std::vector<std::uint8_t> out;
+            while (!go.load()) std::this_thread::yield();
+            std::uint64_t c = 0;
+            while (!stop.load(std::memory_order_relaxed)) {
+                f(t, out);
+                ++c;
+            }
+            calls[t] = c;
+        });
+    const auto t0 = Clock::now();
+    go = true;
+    std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+    stop = true;
+    for (auto& th : ts) th.join();
+    const double el = std::chrono::duration<double>(Clock::now() - t0).count();
+    std::uint64_t total = 0;
+    for (auto c : calls) total += c;
+    std::printf("{\"case\": \"mt_%s\", \"bytes\": %zu, \"threads\": %d, \"calls_per_s\": %.0f, "
+                "\"GB_per_s\": %.4f}\n",
+                name, bytes, threads, total / el, total * (double)bytes / el / 1e9);
     std::fflush(stdout);
 }
 
@@ -94,6 +133,16 @@ std::uint64_t host_loop_pow(const std::array<std::uint8_t, 32>& a, const std::ar
 int main(int argc, char** argv) {
     using namespace ephemeralnet::crypto;
     const int reps = argc > 1 ? std::atoi(argv[1]) : 200;
+    const std::string policy = argc > 2 ? argv[2] : "auto";
+    const int threads = argc > 3 ? std::atoi(argv[3]) : 16;
+#ifdef ENET_BATCH
+    enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
+                                                                                      : ENET_SCALAR_AUTO, 0);
+    std::printf("{\"case\": \"config\", \"build\": \"dropin\", \"policy\": \"%s\", \"host_isa\": \"%s\"}\n",
+                policy.c_str(), enet_host_isa());
+#else
+    std::printf("{\"case\": \"config\", \"build\": \"reference\"}\n");
+#endif
     Key key{};
     for (int i = 0; i < 32; ++i) key.bytes[i] = static_cast<std::uint8_t>(i * 5 + 1);
     Nonce nonce{};
@@ -115,6 +164,31 @@ int main(int argc, char** argv) {
         [&] { g_sink += CryptoManager::encrypt_with_key(key, cid, c4k).data.size(); });
     run("cm_encrypt_with_key", 65536, reps,
         [&] { g_sink += CryptoManager::encrypt_with_key(key, cid, c64k).data.size(); });
+    const auto c1m = pattern(1u << 20, 5), c8m = pattern(8u << 20, 6);
+    // the size sweep that places the AUTO crossover (host engine vs coalesced device path)
+    for (std::size_t sz : {std::size_t(128) << 10, std::size_t(256) << 10, std::size_t(512) << 10,
+                           std::size_t(1) << 20, std::size_t(2) << 20, std::size_t(4) << 20,
+                           std::size_t(8) << 20, std::size_t(32) << 20}) {
+        const std::vector<std::uint8_t> buf(c8m.begin(), c8m.begin() + std::min(sz, c8m.size()));
+        const auto big = sz > c8m.size() ? pattern(sz, 7) : buf;
+        run("chacha20_apply", sz, sz >= (8u << 20) ? 5 : std::max(10, reps / 10),
+            [&] { ChaCha20::apply(key, nonce, big, out, 0); g_sink += out[0]; });
+    }
+    run("sha256_digest", 1u << 20, std::max(10, reps / 10), [&] { g_sink += Sha256::digest(c1m)[0]; });
+
+    // many session threads at once
+    if (threads > 0) {
+        run_mt("hmac_compute", 98, threads, 1.0, [&](int, std::vector<std::uint8_t>&) {
+            g_sink += HmacSha256::compute(key.bytes, m98)[0]; });
+        run_mt("chacha20_apply", 1500, threads, 1.0, [&](int, std::vector<std::uint8_t>& o) {
+            ChaCha20::apply(key, nonce, f1500, o, 0); g_sink += o[0]; });
+        run_mt("chacha20_apply", 65536, threads, 1.0, [&](int, std::vector<std::uint8_t>& o) {
+            ChaCha20::apply(key, nonce, c64k, o, 0); g_sink += o[0]; });
+        run_mt("chacha20_apply", 1u << 20, threads, 1.5, [&](int, std::vector<std::uint8_t>& o) {
+            ChaCha20::apply(key, nonce, c1m, o, 0); g_sink += o[0]; });
+        run_mt("sha256_digest", 65536, threads, 1.0, [&](int, std::vector<std::uint8_t>&) {
+            g_sink += Sha256::digest(c64k)[0]; });
+    }
 
     // handshake PoW at difficulty 8 (about 256 attempts expected), 5 different peers
     std::array<std::uint8_t, 32> pa{}, pb{};
