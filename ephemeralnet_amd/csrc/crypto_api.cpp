@@ -47,9 +47,12 @@
 // ------------------------------------------------------------------------------ scalar routing
 namespace enet::scalar {
 std::atomic<int> g_policy{ENET_SCALAR_AUTO};
-// ChaCha20 records from this size go to the MI355X under ENET_SCALAR_AUTO (INTEGRATION.md
-// measures the crossover: below it the host engine's AVX2 keystream beats PCIe + launch)
-std::atomic<uint64_t> g_crossover{256u << 10};
+// ChaCha20 records from this size go to the MI355X under ENET_SCALAR_AUTO.  Default: never.
+// Measured on the box: the host engine's AVX-512 keystream runs ~10 GB/s per
+// thread, i.e. as fast as the memcpy that moves a pageable caller buffer into pinned memory, so
+// for a caller's std::vector the device round trip never wins; a deployment whose cores are the
+// bottleneck opts in with enet_scalar_set_policy(ENET_SCALAR_AUTO, bytes).
+std::atomic<uint64_t> g_crossover{UINT64_MAX};
 std::atomic<int> g_on_error{0};
 std::atomic<uint64_t> g_failures{0}, g_launches{0}, g_records{0};
 // Per-call counters are sharded over cache lines: one shared atomic incremented by every session
@@ -431,17 +434,22 @@ public:
     }
 
 private:
+    // Records longer than kSeg are cut into kSeg-byte segments, each its own record with start
+    // counter counter + kSeg/64 * k (mod 2^32, as ChaCha20.cpp:110 wraps): one record gets at most
+    // 16 lanes, so a lone 1 MiB record ran on 16 lanes at ~0.5 GB/s.
+    static constexpr size_t kSeg = 16u << 10;
+
     void run(const std::vector<ChachaReq*>& batch) {
-        const size_t n = batch.size();
-        // arena: records back to back | offsets [n+1] | keys [n][32] | nonces [n][12] | counters [n]
-        uint64_t mx = 0, rec = 0;
+        size_t nseg = 0;
+        uint64_t rec = 0;
         for (const ChachaReq* q : batch) {
+            nseg += (q->n + kSeg - 1) / kSeg;
             rec += q->n;
-            mx = std::max<uint64_t>(mx, q->n);
         }
-        const size_t off_at = (rec + 255) & ~size_t(255), keys_at = off_at + 8 * (n + 1),
-                     non_at = keys_at + 32 * n, ctr_at = (non_at + 12 * n + 3) & ~size_t(3),
-                     total = ctr_at + 4 * n;
+        // arena: records back to back | offsets [nseg+1] | keys [nseg][32] | nonces [nseg][12] | counters [nseg]
+        const size_t off_at = (rec + 255) & ~size_t(255), keys_at = off_at + 8 * (nseg + 1),
+                     non_at = keys_at + 32 * nseg, ctr_at = (non_at + 12 * nseg + 3) & ~size_t(3),
+                     total = ctr_at + 4 * nseg;
         if (total > cap_) {
             if (arena_) (void)hipHostFree(arena_);
             arena_ = nullptr;
@@ -455,17 +463,21 @@ private:
         }
         uint64_t* offs = reinterpret_cast<uint64_t*>(arena_ + off_at);
         uint64_t o = 0;
-        for (size_t i = 0; i < n; ++i) {
-            offs[i] = o;
-            std::memcpy(arena_ + o, batch[i]->in, batch[i]->n);
-            o += batch[i]->n;
-            std::memcpy(arena_ + keys_at + 32 * i, batch[i]->key, 32);
-            std::memcpy(arena_ + non_at + 12 * i, batch[i]->nonce, 12);
-            std::memcpy(arena_ + ctr_at + 4 * i, &batch[i]->counter, 4);
+        size_t k = 0;
+        for (const ChachaReq* q : batch) {
+            std::memcpy(arena_ + o, q->in, q->n);
+            for (size_t at = 0; at < q->n; at += kSeg, ++k) {
+                offs[k] = o + at;
+                std::memcpy(arena_ + keys_at + 32 * k, q->key, 32);
+                std::memcpy(arena_ + non_at + 12 * k, q->nonce, 12);
+                const uint32_t c = q->counter + (uint32_t)(at / 64);  // u32 wrap
+                std::memcpy(arena_ + ctr_at + 4 * k, &c, 4);
+            }
+            o += q->n;
         }
-        offs[n] = o;
+        offs[nseg] = o;
         enet_records r{};
-        r.count = (uint32_t)n;
+        r.count = (uint32_t)nseg;
         r.in_offsets = reinterpret_cast<const uint64_t*>(dev_ + off_at);
         r.out_offsets = r.in_offsets;
         r.in = dev_;
@@ -474,17 +486,17 @@ private:
         r.key_stride = 32;
         r.nonces = dev_ + non_at;
         r.total_bytes_hint = rec;
-        r.max_len_hint = (uint32_t)std::min<uint64_t>(mx, 0xffffffffu);
+        r.max_len_hint = (uint32_t)std::min<uint64_t>(rec, kSeg);
         enet_check(enet_chacha20_xor_batch(&r, reinterpret_cast<const uint32_t*>(dev_ + ctr_at), st_.s()),
                    "chacha20 (coalesced)");
         hip_check(hipStreamSynchronize(st_.s()), "hipStreamSynchronize");
         o = 0;
-        for (size_t i = 0; i < n; ++i) {
-            std::memcpy(batch[i]->out, arena_ + o, batch[i]->n);
-            o += batch[i]->n;
+        for (const ChachaReq* q : batch) {
+            std::memcpy(q->out, arena_ + o, q->n);
+            o += q->n;
         }
         scalar::g_launches.fetch_add(1, std::memory_order_relaxed);
-        scalar::g_records.fetch_add(n, std::memory_order_relaxed);
+        scalar::g_records.fetch_add(batch.size(), std::memory_order_relaxed);
     }
 
     std::mutex mu_;

@@ -273,15 +273,19 @@ ENET_API int enet_set_staging(int variant);
  * The reference signatures take ONE record per call from many session threads
  * (SessionManager.cpp:332,703) and never throw.  A GPU round trip costs >= ~18 us,
  * and SHA-256 of one message is one serial chain, so the drop-in routes each call by size:
- *   ENET_SCALAR_AUTO (default)  SHA-256 / HMAC / single PoW checks and ChaCha20 records below the
- *                               crossover run on the calling thread's host engine (SHA-NI / AVX2,
- *                               csrc/host_engine.cpp); ChaCha20 records at or above it go to the
- *                               MI355X, concurrent callers coalesced into one launch; PoW
- *                               searches and KeyManager::rotate_all_due run on the MI355X.
+ *   ENET_SCALAR_AUTO (default)  SHA-256 / HMAC / single PoW checks, and ChaCha20 records below
+ *                               the crossover, run on the calling thread's host engine (SHA-NI,
+ *                               AVX-512 / AVX2; csrc/host_engine.cpp); ChaCha20 records at or
+ *                               above it go to the MI355X, concurrent callers coalesced into one
+ *                               launch through a pinned arena; PoW searches and
+ *                               KeyManager::rotate_all_due run on the MI355X.  The default
+ *                               crossover is UINT64_MAX (never): measured on the box, the host
+ *                               engine's keystream (~10 GB/s per thread) is as fast as the memcpy
+ *                               a pageable caller buffer needs to reach the device at all.
  *   ENET_SCALAR_DEVICE          every call that has a device kernel runs on the MI355X (round-2
  *                               behaviour; the streaming Sha256 class stays on the host).
  *   ENET_SCALAR_HOST            everything on the host engine.
- * crossover_bytes = 0 keeps the current value (default 262144).  A failed device call of the
+ * crossover_bytes = 0 keeps the current value.  A failed device call of the
  * scalar API is finished on the host engine (bit-exact), counted in device_failures and reported
  * once on stderr -- or, after enet_scalar_set_on_device_error(1), abort()s.  No exception ever
  * leaves a reference signature except std::bad_alloc.  The batch entry points (this header's

@@ -158,7 +158,7 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         expect.append(("eq", f"{c['ct']['hex'] or '-'} {c['tag']}"))
     # every policy: the device (each call one GPU round trip), auto with a 1-byte crossover (every
     # ChaCha20 record through the coalescer), the default auto and the host engine
-    for pol in ("policy device", "policy auto 1", "policy auto 262144", "policy host"):
+    for pol in ("policy device", "policy auto 1", "policy auto 0", "policy host"):
         res, err = run_ops(api_bin, [pol, "reset_stats"] + ops + ["stats"])
         assert res[:2] == ["0", "ok"], pol
         check(ops, expect, res[2:-1])
