@@ -117,6 +117,17 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
     if (cipher && Ts) atomicMax(&tmax_s, Ts);
     __syncthreads();
     const uint32_t Tmax = __builtin_amdgcn_readfirstlane(tmax_s);
+    // Length-graded issue priority: a workgroup lasts as long as its longest record's serial
+    // SHA-256 chain (one lane; 64 KiB = 1 027 compressions, ~2.8 ms), so with mixed lengths (C5)
+    // the kernel's tail is that chain -- and when other workgroups (or, with overlapped steps, the
+    // other direction's kernel) share its SIMDs, the chain only gets its share of issue slots.
+    // Both waves of a long workgroup are on that chain (they meet at every stage barrier), so
+    // they win arbitration over shorter workgroups'.
+    if (p.prio == 0) {
+        if (Tmax >= 256) __builtin_amdgcn_s_setprio(3);
+        else if (Tmax >= 64) __builtin_amdgcn_s_setprio(2);
+        else if (Tmax >= 16) __builtin_amdgcn_s_setprio(1);
+    }
 
     // 16-byte chunk swizzles (row = record rl): conflict-free ds_write_b128 (8-lane groups) and
     // ds_read_b128 (16-lane groups) for the 128-byte runs and the 32-byte tail extension
