@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps; MI355X clocks ramp over the first ~10 ms of sustained load")
-    ap.add_argument("--records", type=int, default=65536)
+    ap.add_argument("--records", type=int, default=None,
+                    help="records per GPU (default 65 536; --c5: 524 288, BASELINE config 5)")
     ap.add_argument("--record-bytes", type=int, default=4096)
     ap.add_argument("--lanes", type=int, default=0, help="force lanes per record (0 = scheduler)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -98,7 +99,11 @@ def parse():
                     help="aead = seal+open (headline); xor = ChaCha20-only pass pair (roofline "
                          "probe); wire = session wire frames seal+open (SURVEY 8f row 1, messages "
                          "of --record-bytes); store = chunk store+fetch pipeline (8f row 2)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.records_given = a.records is not None
+    if a.records is None:
+        a.records = 65536
+    return a
 
 
 def host_threads() -> int:
@@ -376,7 +381,8 @@ def c5(args) -> dict:
     if world > 1:
         dev, red_dev = dist_init(local)
     rng = np.random.default_rng(5)
-    n_all = args.records * world
+    # BASELINE config 5: n = 524 288 records (~7 GB) unless --records says otherwise
+    n_all = (args.records if args.records_given else 524288) * world
     lens_all = np.exp(rng.uniform(np.log(512), np.log(65536), n_all)).astype(np.int64)
     lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
     lens = lens_all[lo:hi]
@@ -453,6 +459,7 @@ def c5_device(args) -> dict:
     keys = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, device=dev, generator=g)
     nonces = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, device=dev, generator=g)
     dl = offs[1:] - offs[:-1]
+    mx = int(lens.max())  # host-known hints, as a caller that built the batch has them
     # --c5-overlap: consecutive steps overlap -- step k+1's seal runs beside step k's open (two
     # streams; an open waits only for its own seal), so the serial HMAC chain of one step's
     # longest records (~2.8 ms for 64 KiB, one lane) hides under the other direction's work.
@@ -475,7 +482,8 @@ def c5_device(args) -> dict:
         with torch.cuda.stream(s_seal):
             order = (torch.argsort(dl, descending=True).to(torch.int32)
                      if args.c5_order == "sorted" else None)
-            E.aead_hmac_seal(E.Batch(pt, offs, keys, nonces, order=order), ct[b], tags[b], macs[b])
+            E.aead_hmac_seal(E.Batch(pt, offs, keys, nonces, order=order, total_bytes_hint=total,
+                                     max_len_hint=mx), ct[b], tags[b], macs[b])
             sealed = torch.cuda.Event()
             sealed.record(s_seal)
         if order is not None:
@@ -483,7 +491,8 @@ def c5_device(args) -> dict:
         order_holder[b] = order  # keep the order tensor alive until the open has run
         with torch.cuda.stream(s_open):
             s_open.wait_event(sealed)
-            E.aead_hmac_open(E.Batch(ct[b], offs, keys, nonces, order=order), back[b], tags[b], macs[b], ok[b])
+            E.aead_hmac_open(E.Batch(ct[b], offs, keys, nonces, order=order, total_bytes_hint=total,
+                                     max_len_hint=mx), back[b], tags[b], macs[b], ok[b])
 
     # parity buffers: seal k+2 rewrites ct[b] / tags[b] / macs[b], which open k reads -- each
     # seal waits for the open two steps back

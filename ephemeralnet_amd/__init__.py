@@ -56,7 +56,8 @@ EXPORTS = [
     "enet_wire_open_batch", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
-    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_last_error",
+    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split",
+    "enet_last_error",
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
     "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_host_alloc",
@@ -102,6 +103,7 @@ def lib() -> C.CDLL:
         L.enet_lanes_per_record.restype = u32
         L.enet_set_lanes_per_record.argtypes = [u32]
         L.enet_set_staging.argtypes = [C.c_int]
+        L.enet_set_duplex_split.argtypes = [C.c_int]
         L.enet_last_error.restype = C.c_char_p
         L.enet_pipeline_create.argtypes = [C.c_int, u64, u32]
         L.enet_pipeline_create.restype = vp
@@ -326,6 +328,12 @@ def set_staging(variant: int) -> None:
     """Uniform-batch staging variant: 1 register prefetch (default), 3 LDS DMA / four waves per
     SIMD, 0 per-lane path only, -1 restores the default (results are identical)."""
     _check(lib().enet_set_staging(variant), "enet_set_staging")
+
+
+def set_duplex_split(mode: int) -> None:
+    """Chunk / AEAD+HMAC duplex paths: 1 = split each record over cipher, schedule and rounds
+    waves, 0 = one cipher + one hash lane, -1 = automatic (longest record >= 16 KiB)."""
+    _check(lib().enet_set_duplex_split(mode), "enet_set_duplex_split")
 
 
 def make_batch(items: Sequence[bytes], keys: Sequence[bytes], nonces: Sequence[bytes],

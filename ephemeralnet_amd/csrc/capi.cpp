@@ -141,6 +141,7 @@ enet::DuplexParams duplex_params(const enet_records* r) {
     p.nonces = r->nonces;
     p.order = r->order;
     p.uniform = r->max_len_hint && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint;
+    p.max_len = r->max_len_hint;
     return p;
 }
 
@@ -156,6 +157,9 @@ void set_last_error(const std::string& what) { g_last_error = what; }
 
 static std::atomic<uint32_t> g_forced_lanes{0};
 static std::atomic<uint32_t> g_staging{0};
+static std::atomic<int> g_duplex_split{-1};
+
+int duplex_split_mode() { return g_duplex_split.load(std::memory_order_relaxed); }
 
 // Uniform-batch staging: 1 = register prefetch + LDS transposition (default), 3 = LDS DMA,
 // one live keystream block, four waves per SIMD; 0 = per-lane path only.  ENET_COOP /
@@ -217,6 +221,12 @@ int enet_set_staging(int variant) {
     if (variant != -1 && variant != 0 && variant != 1 && variant != 3 && variant != 4 && variant != 5)
         return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 3, 4 or 5");
     enet::g_staging.store((uint32_t)(variant + 1), std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+int enet_set_duplex_split(int mode) {
+    if (mode != -1 && mode != 0 && mode != 1) return fail(ENET_EINVAL, "duplex split mode must be -1, 0 or 1");
+    enet::g_duplex_split.store(mode, std::memory_order_relaxed);
     return ENET_OK;
 }
 

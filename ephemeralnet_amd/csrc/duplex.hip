@@ -481,6 +481,15 @@ hipError_t launch_duplex_rpw(int kind, bool open, const DuplexParams& p, hipStre
 
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
+    // long records (a 64 KiB record's serial hash chain is the whole kernel time): chunks and
+    // AEAD + HMAC split each record over three waves (duplex_split.hip)
+    if (kind == DK_CHUNK || kind == DK_AEADH) {
+        const int m = duplex_split_mode();
+        if (m == 1 || (m == -1 && p.max_len >= 16384u)) {
+            DuplexParams q = p;
+            return launch_duplex_split(kind, open, q, s);
+        }
+    }
     static const int prio_env = [] {
         const char* e = std::getenv("ENET_DUPLEX_PRIO");
         return e ? (int)std::strtol(e, nullptr, 10) : 0;

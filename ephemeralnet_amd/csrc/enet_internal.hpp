@@ -112,9 +112,16 @@ struct DuplexParams {
     const uint8_t* tags_in;    // AEADH open: expected tags
     uint8_t* ok;               // open / fetch verdicts
     int uniform;               // host hint: every record the same length (scheduling only)
-    int prio;                  // issue priority: 1 = hash waves first, 2 = cipher waves first
+    uint32_t max_len;          // host hint: longest record (scheduling only; 0 = unknown)
+    int prio;                  // issue priority: 0 = length-graded (default), -1 = none,
+                               // 1 = hash waves first, 2 = cipher waves first
 };
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s);
+// chunk / AEAD+HMAC kinds with each record's work split over cipher, schedule and rounds waves
+// (duplex_split.hip): a shorter serial chain for long records
+hipError_t launch_duplex_split(int kind, bool open, const DuplexParams& p, hipStream_t s);
+// -1 auto (split when the longest record is >= 16 KiB), 0 never, 1 always (chunk / AEADH kinds)
+int duplex_split_mode();
 
 // Proof-of-work search / check (pow.hip): SHA-256(prefix_i || BE64(candidate)).
 struct PowParams {

@@ -276,9 +276,18 @@ def test_wire_frames_full_c3_roundtrip(enet, n, L):
     assert torch.count_nonzero(back[(n - 3) * L:(n - 2) * L]).item() == 0
 
 
+@pytest.fixture(params=[-1, 0, 1], ids=["split-auto", "split-off", "split-on"])
+def split(enet, request):
+    """Chunk and AEAD+HMAC duplex paths with each record split over cipher / schedule / rounds
+    waves (duplex_split.hip) forced on, off, or automatic (longest record >= 16 KiB)."""
+    enet.set_duplex_split(request.param)
+    yield request.param
+    enet.set_duplex_split(-1)
+
+
 # ------------------------------------------------------------------------------ chunks
 @pytest.mark.parametrize("L,n,base", [(4000, 300, 0), (100, 260, 3), (65536, 40, 0), (4096, 300, 1)])
-def test_ragged_chunks_vs_oracle(enet, L, n, base):
+def test_ragged_chunks_vs_oracle(enet, split, L, n, base):
     """Chunk store / fetch with given ids at ragged and 64 KiB lengths: ciphertext from counter
     LE32(id), digests = SHA-256(pt), fetch verifies and zeroes a tampered chunk; two-pass agrees."""
     import torch
@@ -324,7 +333,7 @@ def test_ragged_chunks_vs_oracle(enet, L, n, base):
 
 # ------------------------------------------------------------------------------ AEAD + HMAC (C5)
 @pytest.mark.parametrize("sort", [False, True])
-def test_aead_hmac_c5_mixed_vs_oracle(enet, sort):
+def test_aead_hmac_c5_mixed_vs_oracle(enet, split, sort):
     """C5 shape (log-uniform 512 B - 64 KiB) in one pass, optionally length-sorted through
     `order`: tags and HMACs bit-exact, open verifies both, either tampering zeroes the record;
     the two-pass path agrees."""
@@ -378,3 +387,88 @@ def test_aead_hmac_c5_mixed_vs_oracle(enet, sort):
             assert ok[i] == 0 and got[i] == bytes(lens[i]), i
         else:
             assert ok[i] == 1 and got[i] == items[i], i
+
+
+# every ragged-end shape of the split kernel: tail 0..127 bytes (1, 2 or 3 final SHA-256 blocks:
+# r + 9 <= 64, <= 128, > 128), whole stages, empty records, a record of the wrong output size
+EDGE_LENS = [0, 1, 15, 16, 55, 56, 63, 64, 65, 119, 120, 127, 128, 129, 183, 184, 191, 192, 255, 256,
+             257, 383, 1000, 1500, 4095, 4096, 16384, 20000 + 37, 65536]
+
+
+@pytest.mark.parametrize("kind", ["chunk", "aeadh"])
+@pytest.mark.parametrize("base", [0, 3])
+def test_split_kernel_edge_lengths_vs_oracle(enet, kind, base):
+    """duplex_split.hip forced on: bit-exact ciphertext, SHA-256 / HMAC and Poly1305 tags for
+    every tail shape, in-order and reversed (caller order); open verifies and rejects a flipped
+    last byte per record shape; a record whose output range is the wrong size is zeroed (ok 0)."""
+    import hashlib
+    import torch
+    enet.set_duplex_split(1)
+    try:
+        lens = EDGE_LENS * 3
+        n = len(lens)
+        items = [splitmix_bytes(71000 + i, L) for i, L in enumerate(lens)]
+        keys = [splitmix_bytes(72000 + i, 32) for i in range(n)]
+        nonces = [splitmix_bytes(73000 + i, 12) for i in range(n)]
+        ids = [splitmix_bytes(74000 + i, 32) for i in range(n)]
+        b = enet.make_batch(items, keys, nonces, base_offset=base)
+        order = torch.tensor(list(range(n))[::-1], dtype=torch.int32, device="cuda")
+        b = dataclasses.replace(b, order=order)
+        idt = torch.frombuffer(bytearray(b"".join(ids)), dtype=torch.uint8).cuda()
+        offs = b.offsets.cpu().tolist()
+        out = torch.zeros_like(b.arena)
+        d1 = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+        d2 = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+        if kind == "chunk":
+            enet.chunk_store(b, out, d2, chunk_ids=idt)
+        else:
+            enet.aead_hmac_seal(b, out, d1, d2)
+        cts = records_of(host(out), offs)
+        h1, h2 = host(d1), host(d2)
+        for i in range(n):
+            if kind == "chunk":
+                ctr = int.from_bytes(ids[i][:4], "little")
+                assert cts[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], ctr), (i, lens[i])
+                assert h2[32 * i:32 * i + 32] == hashlib.sha256(items[i]).digest(), (i, lens[i])
+            else:
+                c, t = oracle.aead_seal(keys[i], nonces[i], items[i])
+                assert cts[i] == c and h1[16 * i:16 * i + 16] == t, (i, lens[i])
+                assert h2[32 * i:32 * i + 32] == oracle.hmac_sha256(keys[i], items[i]), (i, lens[i])
+        # open: flip the last byte of every third non-empty record
+        cta = torch.frombuffer(bytearray(host(out)), dtype=torch.uint8).cuda()
+        bad = {i for i in range(0, n, 3) if lens[i] > 0}
+        for i in bad:
+            cta[offs[i] + lens[i] - 1] ^= 0x40
+        b2 = dataclasses.replace(b, arena=cta)
+        back = torch.full_like(b.arena, 0x77)
+        ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        if kind == "chunk":
+            enet.chunk_fetch(b2, back, idt, d2, ok)
+        else:
+            enet.aead_hmac_open(b2, back, d1, d2, ok)
+        got = records_of(host(back), offs)
+        okl = ok.cpu().tolist()
+        for i in range(n):
+            if i in bad:
+                assert okl[i] == 0 and got[i] == bytes(lens[i]), (i, lens[i])
+            else:
+                assert okl[i] == 1 and got[i] == items[i], (i, lens[i])
+        # wrong output size (AEAD + HMAC seal): record 7's output range one byte short -> zeroed
+        ooffs = np.array(offs, dtype=np.int64)
+        ooffs[8:] -= 1
+        o2 = torch.full((int(ooffs[-1]) + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+        tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+        macs = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+        r = dataclasses.replace(b, order=None).records(o2, torch.tensor(ooffs).cuda())
+        import ctypes as C
+        if kind == "aeadh":
+            assert enet.lib().enet_aead_hmac_seal_batch(C.byref(r), enet._ptr(tags), enet._ptr(macs),
+                                                        enet._stream(None)) == 0
+            ob = host(o2)
+            seg = records_of(ob, ooffs.tolist())
+            assert seg[7] == bytes(len(seg[7]))
+            for i in (6, 9, 20):
+                c, t = oracle.aead_seal(keys[i], nonces[i], items[i])
+                assert seg[i] == c, i
+    finally:
+        enet.set_duplex_split(-1)

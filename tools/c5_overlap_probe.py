@@ -42,7 +42,8 @@ def seal(x, s=None):
 
 
 def opn(x, s=None):
-    bo = E.Batch(x["ct"], x["offs"], x["keys"], x["nonces"], order=x["order"])
+    bo = E.Batch(x["ct"], x["offs"], x["keys"], x["nonces"], order=x["order"],
+                 total_bytes_hint=x["b"].total_bytes_hint, max_len_hint=x["b"].max_len_hint)
     E.aead_hmac_open(bo, x["back"], x["tags"], x["macs"], x["ok"], stream=s)
 
 
