@@ -45,7 +45,8 @@ STALL_PASSES = [
 
 
 def kernel_key(name: str):
-    if not any(k in name for k in ("records_kernel", "sha_kernel", "stream_kernel", "duplex_kernel")):
+    if not any(k in name for k in ("records_kernel", "sha_kernel", "stream_kernel", "duplex_kernel",
+                                   "duplex_split_kernel")):
         return None
     return name.split("(")[0].replace("void ", "")
 
