@@ -332,7 +332,8 @@ def set_staging(variant: int) -> None:
 
 def set_duplex_split(mode: int) -> None:
     """Chunk / AEAD+HMAC duplex paths: 1 = split each record over cipher, schedule and rounds
-    waves, 0 = one cipher + one hash lane, -1 = automatic (longest record >= 16 KiB)."""
+    waves, 0 = one cipher + one hash lane, -1 = automatic (longest record >= 16 KiB in a uniform
+    or caller-ordered batch)."""
     _check(lib().enet_set_duplex_split(mode), "enet_set_duplex_split")
 
 

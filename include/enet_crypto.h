@@ -321,8 +321,8 @@ ENET_API void enet_host_hmac_sha256(const uint8_t* key, uint64_t key_len, const 
 /* Duplex paths with a hash beside the cipher (chunk store / fetch with ids, AEAD + HMAC): long
  * records run with each record's work split over a cipher, a SHA-256 schedule and a SHA-256
  * rounds wave (a ~1.4x shorter serial chain, duplex_split.hip).  -1 = automatic (when
- * max_len_hint >= 16 KiB, the default), 0 = never, 1 = always.  Results are identical;
- * tuning / test knob. */
+ * max_len_hint >= 16 KiB and the batch is uniform or has an `order`, e.g. length-sorted; the
+ * default), 0 = never, 1 = always.  Results are identical; tuning / test knob. */
 ENET_API int enet_set_duplex_split(int mode);
 /* Human-readable text of the last error on this host thread ("" if none). */
 ENET_API const char* enet_last_error(void);
