@@ -53,6 +53,9 @@ step pmc
 timeout -k 10 600 python tools/pmc.py --out $O/pmc --summary $O/pmc_summary.json --config "{\"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --no-power --steps 3 --warmup 1 > $O/pmc.log 2>&1
 timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3 --summary $O/pmc_c3_summary.json --config "{\"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --no-power --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3.log 2>&1
 timeout -k 10 600 python tools/pmc.py --out $O/pmc_c3w --summary $O/pmc_c3w_summary.json --config "{\"mode\": \"wire\", \"records\": 1048576, \"record_bytes\": 1500}" -- python3 bench.py --no-cpu-baseline --no-power --mode wire --records 1048576 --record-bytes 1500 --steps 2 --warmup 1 > $O/pmc_c3w.log 2>&1
+# calibration of FETCH_SIZE for the duplex kernel's per-lane 16-byte access pattern: chunks of
+# 4096 B at 128-byte-aligned starts read and write exactly 2 x 256 MiB + ids/keys per launch
+timeout -k 10 600 python tools/pmc.py --out $O/pmc_st --summary $O/pmc_st_summary.json --config "{\"mode\": \"store\", \"records\": 65536, \"record_bytes\": 4096}" -- python3 bench.py --no-cpu-baseline --no-power --mode store --steps 2 --warmup 1 > $O/pmc_st.log 2>&1
 timeout -k 10 600 python tools/pmc.py --out $O/pmc_c5 --summary $O/pmc_c5_summary.json --config "{\"workload\": \"C5 device\", \"records\": 65536}" -- python3 bench.py --no-power --c5-device --records 65536 --steps 2 --warmup 1 > $O/pmc_c5.log 2>&1
 fi
 step done
