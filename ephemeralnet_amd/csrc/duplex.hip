@@ -482,7 +482,7 @@ hipError_t launch_duplex_rpw(int kind, bool open, const DuplexParams& p, hipStre
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s) {
     if (p.n == 0) return hipSuccess;
     // long records (a 64 KiB record's serial hash chain is the whole kernel time): chunks and
-    // AEAD + HMAC split each record over three waves (duplex_split.hip) -- for uniform batches
+    // AEAD + HMAC split each record over four waves (duplex_split.hip) -- for uniform batches
     // and batches the caller ordered (length-sorted, like C5).  The split kernel holds 2
     // workgroups per CU (80 KiB LDS) against 6 here, so an UNSORTED mixed batch, where every
     // workgroup holds some long record, runs two rounds of chains there: 45 vs 69 GiB/s at C5.

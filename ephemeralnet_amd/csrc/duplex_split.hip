@@ -1,5 +1,5 @@
 // duplex_split.hip -- the duplex pass (cipher + hash, one HBM pass) for LONG records, with the
-// per-record work split over three waves so that a record's serial chain is shorter (gfx950).
+// per-record work split over four waves so that a record's serial chain is shorter (gfx950).
 //
 // Why: in duplex.hip a record has one cipher lane and one hash lane; SHA-256 is serial inside a
 // record, so a workgroup lasts as long as its longest record's chain: per 128-byte stage one
@@ -7,15 +7,19 @@
 // runs two ChaCha20 blocks + Poly1305 (~2 330), and a lone wave issues one VALU instruction per
 // ~4.5 cycles.  A 64 KiB record is 512 stages: 2.63 ms measured (tools/c5_overlap_probe.py) --
 // the whole time of a C5 batch (BASELINE config 5: mixed 512 B-64 KiB, VALU busy 31 %) and of a
-// 64 KiB chunk store.  Here lane l of three waves serves record l of the workgroup:
-//   C (wave 0)  ChaCha20: loads the run, keystream, stores; hands the ciphertext (seal) or the
-//               plaintext (open) of each stage to S through an LDS run slab;
-//   S (wave 1)  the SHA-256 message schedule W[0..63] of the stage's two blocks (plaintext: seal
+// 64 KiB chunk store.  Here lane l of four waves serves record l of the workgroup:
+//   C0, C1 (waves 0, 1)  ChaCha20, one 64-byte block of the stage each: load, keystream, store;
+//               they hand the ciphertext (seal) or the plaintext (open) of each stage to S
+//               through an LDS run slab;
+//   S (wave 2)  the SHA-256 message schedule W[0..63] of the stage's two blocks (plaintext: seal
 //               re-loads the input run, an L2 hit; open takes C's output) into an LDS W slab, and
 //               Poly1305 over the ciphertext (AEAD; seal from C's slab, open re-loads the input);
-//   R (wave 2)  the 64 SHA-256 rounds per block over the W slab, and the digest / HMAC finish.
+//   R (wave 3)  the 64 SHA-256 rounds per block over the W slab, and the digest / HMAC finish.
 // Stage u is ciphered in interval u, scheduled in u + 1 and hashed in u + 2 (one workgroup
-// barrier per interval); the chain per stage becomes max(C ~1 960, S ~1 350, R ~1 830).
+// barrier per interval); VALU instructions per stage: C0 / C1 ~1 000 each, S ~1 350 (AEAD),
+// R 1 808 (14 per round, the floor), so R is the chain: 64 KiB in 1.90 ms.  (Three waves, one C
+// for both blocks at ~1 960, measured the same chain: R bound it already.  The fourth wave raised
+// the throughput around it: C5 device-resident 170 -> 192 GiB/s.)
 // The ragged end (< 128 bytes) follows the same three steps: C encrypts and stores the tail, S
 // finishes Poly1305 (tag) and lays out the padded final SHA-256 blocks (message tail, 0x80,
 // BE64 bit length: 1-3 blocks), R compresses them, finishes HMAC (opad) and writes the digest /
@@ -34,7 +38,8 @@ namespace enet {
 namespace {
 
 constexpr uint32_t kSRun = 128;  // bytes per stage and record
-constexpr uint32_t kSRec = 64;   // records per workgroup (one lane each in 3 waves)
+constexpr uint32_t kSRec = 64;   // records per workgroup (one lane each in 4 waves)
+constexpr uint32_t kSWaves = 4;  // C0, C1, S, R
 
 #define ENET_SP_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
@@ -75,7 +80,7 @@ __device__ __forceinline__ void sha256_round(uint32_t& a, uint32_t& b, uint32_t&
 }  // namespace
 
 template <int KIND, bool OPEN>
-__global__ __launch_bounds__(3 * kSRec) void duplex_split_kernel(DuplexParams p) {
+__global__ __launch_bounds__(kSWaves * kSRec) void duplex_split_kernel(DuplexParams p) {
     constexpr bool kAead = KIND == DK_AEADH;
     // LDS (conflict-free: chunk-major, one 16-byte chunk per record per row, so a wave's
     // ds_read/write_b128 of chunk c touches 1 KiB contiguous)
@@ -128,19 +133,23 @@ __global__ __launch_bounds__(3 * kSRec) void duplex_split_kernel(DuplexParams p)
         for (int i = 0; i < 8; ++i) kw[i] = live ? reinterpret_cast<const uint32_t*>(kp)[i] : 0u;
     }
 
-    if (wave == 0) {
-        // ================================================================ C: ChaCha20
+    if (wave < 2) {
+        // ================================================================ C0 / C1: ChaCha20
+        // wave hb owns block hb of every stage: bytes [128 t + 64 hb, 128 t + 64 hb + 64)
+        const uint32_t hb = wave;
         uint32_t nw[3];
 #pragma unroll
         for (int i = 0; i < 3; ++i) nw[i] = live ? ld32(p.nonces + 12ull * rec + 4 * i) : 0u;
         ChachaRecord R;
         chacha_record_init(R, kw, nw);
-        const uint32_t c0 = KIND == DK_CHUNK ? (live ? ld32(p.chunk_ids + 32ull * rec) : 0u) : 1u;
-        uint32_t pf[32];
-        auto load_run = [&](uint32_t s) {
-            const uint4* q = reinterpret_cast<const uint4*>(src + (uint64_t)kSRun * s);
+        const uint32_t c0 = (KIND == DK_CHUNK ? (live ? ld32(p.chunk_ids + 32ull * rec) : 0u) : 1u) + hb;
+        const uint8_t* hsrc = src + 64u * hb;
+        uint8_t* hdst = dst + 64u * hb;
+        uint32_t pf[16];
+        auto load_blk = [&](uint32_t s) {
+            const uint4* q = reinterpret_cast<const uint4*>(hsrc + (uint64_t)kSRun * s);
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < 4; ++i) {
                 const uint4 v = q[i];
                 pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
             }
@@ -148,47 +157,47 @@ __global__ __launch_bounds__(3 * kSRec) void duplex_split_kernel(DuplexParams p)
         // the slab carries what S cannot re-load from the input: seal ciphertext (AEAD only:
         // Poly1305 runs over it), open plaintext (the hash input)
         constexpr bool kHand = OPEN || kAead;
-        if (Ts > 0) load_run(0);
+        if (Ts > 0) load_blk(0);
         for (uint32_t t = 0; t < nint; ++t) {
             if (t < Ts) {
-                uint32_t x[32];
+                uint32_t x[16];
 #pragma unroll
-                for (int i = 0; i < 32; ++i) x[i] = pf[i];
-                if (t + 1 < Ts) load_run(t + 1);
+                for (int i = 0; i < 16; ++i) x[i] = pf[i];
+                if (t + 1 < Ts) load_blk(t + 1);
                 {
-                    uint32_t ka[16], kb[16];
-                    chacha_block2(R, c0 + 2u * t, c0 + 2u * t + 1u, ka, kb);
+                    uint32_t ka[16];
+                    chacha_block(R, c0 + 2u * t, ka);
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
+                    for (int i = 0; i < 16; ++i) x[i] ^= ka[i];
                 }
-                uint4* o = reinterpret_cast<uint4*>(dst + (uint64_t)kSRun * t);
+                uint4* o = reinterpret_cast<uint4*>(hdst + (uint64_t)kSRun * t);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+                for (int i = 0; i < 4; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
                 if (kHand) {
 #pragma unroll
-                    for (int c = 0; c < 8; ++c)
-                        runs[t & 1u][c][lane] = make_uint4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
+                    for (int c = 0; c < 4; ++c)
+                        runs[t & 1u][4 * hb + c][lane] = make_uint4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
                 }
             } else if (t == Ts && valid) {
-                // ragged end: r < 128 bytes, 16-byte windows ending at the record end
-                uint32_t w[32];
+                // ragged end: r < 128 bytes; this wave's part is [64 hb, min(r, 64 hb + 64)), read
+                // through 16-byte windows ending at the record end
+                uint32_t w[16];
 #pragma unroll
-                for (int i = 0; i < 32; ++i) w[i] = 0u;
-                if (r) {
-                    load_block(src + tb, min(r, 64u), w, tb + min(r, 64u) >= 16u);
-                    if (r > 64u) load_block(src + tb + 64, r - 64u, w + 16, tb + r >= 16u);
-                    uint32_t ka[16], kb[16];
-                    chacha_block2(R, c0 + 2u * Ts, c0 + 2u * Ts + 1u, ka, kb);
+                for (int i = 0; i < 16; ++i) w[i] = 0u;
+                const uint32_t rh = r > 64u * hb ? min(r - 64u * hb, 64u) : 0u;
+                if (rh) {
+                    load_block(hsrc + tb, rh, w, tb + 64u * hb + rh >= 16u);
+                    uint32_t ka[16];
+                    chacha_block(R, c0 + 2u * Ts, ka);
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) { w[i] ^= ka[i]; w[16 + i] ^= kb[i]; }
-                    store_block(dst + tb, min(r, 64u), w);
-                    if (r > 64u) store_block(dst + tb + 64, r - 64u, w + 16);
-                    sp_keep_le(w, 32, r);  // RFC 8439 zero pad / clean hash input
+                    for (int i = 0; i < 16; ++i) w[i] ^= ka[i];
+                    store_block(hdst + tb, rh, w);
+                    sp_keep_le(w, 16, rh);  // RFC 8439 zero pad / clean hash input
                 }
                 if (kHand) {
 #pragma unroll
-                    for (int c = 0; c < 8; ++c)
-                        runs[Ts & 1u][c][lane] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+                    for (int c = 0; c < 4; ++c)
+                        runs[Ts & 1u][4 * hb + c][lane] = make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
                 }
             }
             // a failed open is zeroed by R two intervals later: this wave's stores must be done
@@ -196,7 +205,7 @@ __global__ __launch_bounds__(3 * kSRec) void duplex_split_kernel(DuplexParams p)
             if (OPEN && __builtin_amdgcn_ballot_w64(t == Ts && valid)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             ENET_SP_BARRIER();
         }
-    } else if (wave == 1) {
+    } else if (wave == 2) {
         // ================================================================ S: schedule + Poly1305
         PolyR32 PR{};
         uint32_t h[5] = {0, 0, 0, 0, 0}, pad[4] = {0, 0, 0, 0};
@@ -408,7 +417,7 @@ __global__ __launch_bounds__(3 * kSRec) void duplex_split_kernel(DuplexParams p)
 }
 
 hipError_t launch_duplex_split(int kind, bool open, const DuplexParams& p, hipStream_t s) {
-    const dim3 g((p.n + kSRec - 1) / kSRec), b(3 * kSRec);
+    const dim3 g((p.n + kSRec - 1) / kSRec), b(kSWaves * kSRec);
     switch (kind * 2 + (open ? 1 : 0)) {
         case DK_CHUNK * 2: hipLaunchKernelGGL((duplex_split_kernel<DK_CHUNK, false>), g, b, 0, s, p); break;
         case DK_CHUNK * 2 + 1: hipLaunchKernelGGL((duplex_split_kernel<DK_CHUNK, true>), g, b, 0, s, p); break;
