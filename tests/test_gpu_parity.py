@@ -818,3 +818,69 @@ def test_stream_kernel_unaligned_arenas(enet, ishift, oshift):
     for i in range(0, n, 97):
         assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], 0), i
     enet.set_lanes_per_record(0)
+
+
+@pytest.mark.parametrize("L", [1500, 1436, 1284, 260, 132, 196, 4100])
+@pytest.mark.parametrize("ishift,oshift", [(0, 0), (4, 4), (8, 100), (0, 12), (64, 0), (2, 0), (0, 1)])
+def test_stream_ring_shapes(enet, L, ishift, oshift):
+    """The output-ring streaming kernel (stream_ring.hip: one lane per record, L % 128 != 0, whole
+    512-record workgroups, the rest per lane): record starts at every 4-byte phase of a 64-byte
+    unit, one to 32 stages, tails of 4 to 92 bytes, arenas off alignment (a 2- or 1-byte shift is
+    not 4-byte aligned and takes the per-lane path in-kernel).  Seal bit-exact against the oracle
+    at every record of the first workgroup's edges and a sample, nothing written outside the
+    output arena, open(seal(x)) == x, a tampered record (first, middle and last unit) rejected
+    and zeroed with its neighbours intact, and reference-mode ChaCha20 with counters at the
+    u32 wrap."""
+    import torch
+    enet.set_lanes_per_record(1)
+    enet.set_staging(-1)
+    enet.set_stream_ring(1)
+    n = 1100
+    items = [splitmix_bytes(94000 + i, L) for i in range(n)]
+    keys = [splitmix_bytes(95000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(96000 + i, 12) for i in range(n)]
+    b0 = enet.make_batch(items, keys, nonces)
+    ibig = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    ibig[ishift:ishift + n * L] = b0.arena
+    src = ibig[ishift:ishift + n * L]
+    b = enet.Batch(src, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    obig = torch.full((n * L + 256,), 0x5A, dtype=torch.uint8, device="cuda")
+    out = obig[oshift:oshift + n * L]
+    tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+    enet.aead_seal(b, out, tags)
+    offs = b0.offsets.cpu().tolist()
+    got, th = records_of(host(out), offs), host(tags)
+    idx = sorted(set(list(range(0, 70)) + list(range(440, 580)) + list(range(1000, n)) +
+                     list(range(0, n, 13))))
+    for i in idx:
+        ct, tag = oracle.aead_seal(keys[i], nonces[i], items[i])
+        assert got[i] == ct, (i, L)
+        assert th[16 * i:16 * i + 16] == tag, (i, L)
+    ob = host(obig)
+    assert ob[:oshift] == b"\x5a" * oshift and ob[oshift + n * L:] == b"\x5a" * (256 - oshift)
+    b2 = enet.Batch(out, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    bbig = torch.zeros(n * L + 256, dtype=torch.uint8, device="cuda")
+    back = bbig[ishift:ishift + n * L]
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(b2, back, tags, ok)
+    assert int(ok.sum()) == n and torch.equal(back, src)
+    bad = out.clone()
+    for v, pos in ((3, 0), (300, L // 2), (511, L - 1), (513, 5)):
+        bad[offs[v] + pos] ^= 4
+    b3 = enet.Batch(bad, b0.offsets, b0.keys, b0.nonces, total_bytes_hint=n * L, max_len_hint=L)
+    back.fill_(0xAA)
+    enet.aead_open(b3, back, tags, ok)
+    okh = ok.cpu().tolist()
+    assert [i for i in range(n) if okh[i] == 0] == [3, 300, 511, 513]
+    bh = records_of(host(back), offs)
+    for v in (3, 300, 511, 513):
+        assert bh[v] == bytes(L) and bh[v - 1] == items[v - 1] and bh[v + 1] == items[v + 1], v
+    ctr = np.full(n, 0xFFFFFFF0, dtype=np.uint32)
+    ctr[::3] = np.arange(0, n, 3, dtype=np.uint32)
+    xo = obig[oshift:oshift + n * L]
+    enet.chacha20_xor(b, xo, counters=torch.tensor(ctr.view(np.int32)).cuda())
+    xg = records_of(host(xo), offs)
+    for i in idx[::3]:
+        assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i])), i
+    enet.set_stream_ring(-1)
+    enet.set_lanes_per_record(0)
