@@ -56,7 +56,7 @@ EXPORTS = [
     "enet_wire_open_batch", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
-    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split", "enet_set_stream_ring",
+    "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split",
     "enet_last_error",
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
@@ -104,7 +104,6 @@ def lib() -> C.CDLL:
         L.enet_set_lanes_per_record.argtypes = [u32]
         L.enet_set_staging.argtypes = [C.c_int]
         L.enet_set_duplex_split.argtypes = [C.c_int]
-        L.enet_set_stream_ring.argtypes = [C.c_int]
         L.enet_last_error.restype = C.c_char_p
         L.enet_pipeline_create.argtypes = [C.c_int, u64, u32]
         L.enet_pipeline_create.restype = vp
@@ -336,12 +335,6 @@ def set_duplex_split(mode: int) -> None:
     waves, 0 = one cipher + one hash lane, -1 = automatic (longest record >= 16 KiB in a uniform
     or caller-ordered batch)."""
     _check(lib().enet_set_duplex_split(mode), "enet_set_duplex_split")
-
-
-def set_stream_ring(mode: int) -> None:
-    """Uniform one-lane batches with L % 128 != 0: 1 = output-ring streaming kernel, 0 = line
-    staging, -1 = default (ENET_STREAM_RING)."""
-    _check(lib().enet_set_stream_ring(mode), "enet_set_stream_ring")
 
 
 def make_batch(items: Sequence[bytes], keys: Sequence[bytes], nonces: Sequence[bytes],

@@ -13,10 +13,6 @@
 
 #include "enet_internal.hpp"
 
-namespace enet {
-extern std::atomic<int> g_stream_ring;  // enet_set_stream_ring (-1 = ENET_STREAM_RING)
-}
-
 // nonce(12) || BE32 length (SessionManager.cpp:85-86,376-385)
 constexpr uint32_t kWireHeader = 16;
 
@@ -97,14 +93,6 @@ enet::RecParams rec_params(const enet_records* r) {
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.stream = dflt ? strm : 0;
-    // the output-ring kernel for L % 128 != 0 (stream_ring.hip) is opt-in (ENET_STREAM_RING=1)
-    // until it beats the line-staging records kernel at C3
-    static const int ring = [] {
-        const char* e = std::getenv("ENET_STREAM_RING");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    const int ring_set = enet::g_stream_ring.load(std::memory_order_relaxed);
-    p.ring = ring_set == -1 ? ring : ring_set;
 #ifdef ENET_TOOLS_BUILD
     // Measurement probes of the stream kernel (skip keystream / Poly1305 / stores, clock stamps in
     // tag_out) and its memory-schedule variants.  Only the tools build of the library
@@ -170,7 +158,6 @@ void set_last_error(const std::string& what) { g_last_error = what; }
 static std::atomic<uint32_t> g_forced_lanes{0};
 static std::atomic<uint32_t> g_staging{0};
 static std::atomic<int> g_duplex_split{-1};
-std::atomic<int> g_stream_ring{-1};
 
 int duplex_split_mode() { return g_duplex_split.load(std::memory_order_relaxed); }
 
@@ -240,12 +227,6 @@ int enet_set_staging(int variant) {
 int enet_set_duplex_split(int mode) {
     if (mode != -1 && mode != 0 && mode != 1) return fail(ENET_EINVAL, "duplex split mode must be -1, 0 or 1");
     enet::g_duplex_split.store(mode, std::memory_order_relaxed);
-    return ENET_OK;
-}
-
-int enet_set_stream_ring(int mode) {
-    if (mode != -1 && mode != 0 && mode != 1) return fail(ENET_EINVAL, "stream ring mode must be -1, 0 or 1");
-    enet::g_stream_ring.store(mode, std::memory_order_relaxed);
     return ENET_OK;
 }
 

@@ -48,8 +48,6 @@ struct RecParams {
                     // output): 1 no HBM traffic, 2 no keystream, 4 no Poly1305, 64 no stores,
                     // 128 no DMA, 256 clock stamps
     int var;        // streaming kernel code variant (ENET_STREAM_VAR, tuning)
-    int ring;       // uniform batches with L % 128 != 0, one lane per record: the output-ring
-                    // streaming kernel (stream_ring.hip; opt-in, ENET_STREAM_RING=1)
     uint32_t rec_base;  // first record index of this launch (record = group + rec_base)
     // wire frames (frame modes only): every frame starts with a hdr-byte header
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the
@@ -62,9 +60,6 @@ hipError_t launch_records(int mode, const RecParams& p, uint32_t lanes, hipStrea
 // The streaming kernel (stream.hip): whole 512-thread workgroups of a uniform batch.
 bool stream_eligible(const RecParams& p, uint32_t lanes);
 hipError_t launch_stream(int mode, const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s);
-// The output-ring streaming kernel (stream_ring.hip): 512 one-lane records per workgroup.
-bool stream_ring_eligible(const RecParams& p);
-hipError_t launch_stream_ring(int mode, const RecParams& p, uint32_t blocks, hipStream_t s);
 
 struct ShaParams {
     uint32_t n;

@@ -46,23 +46,6 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (FRAME == FR_NONE && LOGP == 0 && stream_ring_eligible(p)) {
-        // one-lane records of a length that is not a multiple of 128 (C3): the output-ring
-        // streaming kernel over whole 512-record workgroups, the rest per lane
-        const uint32_t full = p.n / 512u;
-        RecParams q = p;
-        q.n = full * 512u;
-        if (hipError_t e = launch_stream_ring(MODE, q, full, s)) return e;
-        const uint32_t rest = p.n - full * 512u;
-        if (rest) {
-            RecParams r = p;
-            r.n = rest;
-            r.rec_base = full * 512u;
-            hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 0>), dim3((rest + kWG - 1) / kWG),
-                               dim3(kWG), 0, s, r);
-        }
-        return hipGetLastError();
-    }
     if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop >= 1) {
         // Cooperative kernels over whole workgroups of records (no dead owners, no store
         // predicates); the remaining records go through the per-lane kernel.

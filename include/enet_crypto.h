@@ -324,11 +324,6 @@ ENET_API void enet_host_hmac_sha256(const uint8_t* key, uint64_t key_len, const 
  * max_len_hint >= 16 KiB and the batch is uniform or has an `order`, e.g. length-sorted; the
  * default), 0 = never, 1 = always.  Results are identical; tuning / test knob. */
 ENET_API int enet_set_duplex_split(int mode);
-/* Uniform batches with one lane per record and a length that is not a multiple of 128 bytes
- * (C3: 1 500-byte frames): 1 = the output-ring streaming kernel (stream_ring.hip), 0 = the
- * line-staging record kernel, -1 = the default (ENET_STREAM_RING=1 selects the ring kernel, else
- * line staging).  Results are identical; tuning / test knob. */
-ENET_API int enet_set_stream_ring(int mode);
 /* Human-readable text of the last error on this host thread ("" if none). */
 ENET_API const char* enet_last_error(void);
 /* ABI version: (major << 16) | minor. */

@@ -822,11 +822,11 @@ def test_stream_kernel_unaligned_arenas(enet, ishift, oshift):
 
 @pytest.mark.parametrize("L", [1500, 1436, 1284, 260, 132, 196, 4100])
 @pytest.mark.parametrize("ishift,oshift", [(0, 0), (4, 4), (8, 100), (0, 12), (64, 0), (2, 0), (0, 1)])
-def test_stream_ring_shapes(enet, L, ishift, oshift):
-    """The output-ring streaming kernel (stream_ring.hip: one lane per record, L % 128 != 0, whole
-    512-record workgroups, the rest per lane): record starts at every 4-byte phase of a 64-byte
-    unit, one to 32 stages, tails of 4 to 92 bytes, arenas off alignment (a 2- or 1-byte shift is
-    not 4-byte aligned and takes the per-lane path in-kernel).  Seal bit-exact against the oracle
+def test_uniform_one_lane_shapes(enet, L, ishift, oshift):
+    """Uniform one-lane batches whose length is not a multiple of 128 (C3 class: line staging over
+    whole workgroups, the rest per lane): record starts at every 4-byte phase of a line, one to 32
+    stages, tails of 4 to 92 bytes, arenas off alignment (in / out phases that differ, or a 2- or
+    1-byte shift, take the per-lane path).  Seal bit-exact against the oracle
     at every record of the first workgroup's edges and a sample, nothing written outside the
     output arena, open(seal(x)) == x, a tampered record (first, middle and last unit) rejected
     and zeroed with its neighbours intact, and reference-mode ChaCha20 with counters at the
@@ -834,7 +834,6 @@ def test_stream_ring_shapes(enet, L, ishift, oshift):
     import torch
     enet.set_lanes_per_record(1)
     enet.set_staging(-1)
-    enet.set_stream_ring(1)
     n = 1100
     items = [splitmix_bytes(94000 + i, L) for i in range(n)]
     keys = [splitmix_bytes(95000 + i, 32) for i in range(n)]
@@ -882,5 +881,4 @@ def test_stream_ring_shapes(enet, L, ishift, oshift):
     xg = records_of(host(xo), offs)
     for i in idx[::3]:
         assert xg[i] == oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i])), i
-    enet.set_stream_ring(-1)
     enet.set_lanes_per_record(0)
