@@ -91,7 +91,14 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     // probe (dbg 16384, tools/stage_probe.py): compute wave 0 stamps the 100 MHz clock and the
     // shader clock at entry, the shader clock at the body start, after every stage barrier S0 and
     // after F1, and both clocks at exit, into the workgroup's tag slots
-    const bool stamp = (p.dbg & 16384) && threadIdx.x == 0 && p.tag_out;
+#ifdef ENET_TOOLS_BUILD
+    const int dbg = p.dbg;
+#else
+    // the shipping build compiles the probes out: a runtime probe branch around the keystream made
+    // the compiler route the state through PHI copies (~50 extra v_mov per stage)
+    constexpr int dbg = 0;
+#endif
+    const bool stamp = (dbg & 16384) && threadIdx.x == 0 && p.tag_out;
     uint64_t* stamps = reinterpret_cast<uint64_t*>(p.tag_out + 16ull * rec);
     if (__builtin_expect(stamp, 0)) {
         stamps[0] = __builtin_amdgcn_s_memrealtime();
@@ -113,7 +120,6 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t B = L >> (6 + LOGP);  // blocks per lane (the host launches L % (128 P) == 0)
     const uint32_t S = B >> 1;           // stages
-    const int dbg = p.dbg;
     const bool mem = !(dbg & 1);
 
     if (!compute) {
@@ -449,7 +455,9 @@ template <int MODE>
 static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s) {
     switch (lanes) {
         case 1: hipLaunchKernelGGL((stream_kernel<0, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
-        case 2:  // memory schedule variants of the C2 shape (ENET_STREAM_VAR, tuning)
+        case 2:
+#ifdef ENET_TOOLS_BUILD
+            // memory schedule variants of the C2 shape (ENET_STREAM_VAR, tools build)
             switch (p.var) {
                 case 1: hipLaunchKernelGGL((stream_kernel<1, MODE, 1>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 case 2: hipLaunchKernelGGL((stream_kernel<1, MODE, 2>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
@@ -459,6 +467,9 @@ static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_
                 case 14: hipLaunchKernelGGL((stream_kernel<1, MODE, 14>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
                 default: hipLaunchKernelGGL((stream_kernel<1, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
             }
+#else
+            hipLaunchKernelGGL((stream_kernel<1, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p);
+#endif
             break;
         case 4: hipLaunchKernelGGL((stream_kernel<2, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
         case 8: hipLaunchKernelGGL((stream_kernel<3, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
