@@ -1,16 +1,19 @@
 // frame_queue.cpp -- the cross-session frame queues of Batch.hpp.
 //
 // Many session threads each submit one frame and block.  Whichever waiting thread finds no flush
-// in flight becomes the leader: it keeps collecting until the queue holds max_frames frames or
-// max_bytes bytes or max_delay has passed, takes what is queued (up to the limits), runs ONE
-// batched pass -- crypto::batch::wire_seal / wire_open on the MI355X -- writes every caller's
-// result into that caller's request and wakes them all.  A request is owned by the thread that
+// in flight becomes the leader: it takes what is queued (up to max_frames / max_bytes; with a
+// positive max_delay it first waits for a size trigger or the deadline), runs ONE batched pass --
+// crypto::batch::wire_seal / wire_open on the MI355X -- writes every caller's result into that
+// caller's request and wakes them all; frames arriving meanwhile form the next batch (group
+// commit).  Under the auto and host policies there is no queue: each thread seals / opens its own
+// frame on the host engine, which measured faster than a device pass for MTU frames (see seal()).  A request is owned by the thread that
 // submitted it (it lives on that thread's stack until `done`), results are matched by request,
 // never by position in some shared buffer, so sessions cannot see each other's frames.
 //
 // Reference: SessionManager::send (src/network/SessionManager.cpp:337-388), receive_loop
 // (:703-854) and protocol::encode_signed / decode_signed (src/protocol/Message.cpp:305-328).
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -56,9 +59,14 @@ public:
                 continue;
             }
             busy_ = true;
-            // collect until a size trigger or the deadline
-            const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
-            while (!full() && more_.wait_until(lk, deadline) != std::cv_status::timeout) {
+            // group commit: frames that arrive while a flush runs queue up for the next leader, so
+            // under load the batch grows with the flush time and no deadline is needed (max_delay
+            // 0, the default).  A positive max_delay makes the leader also wait for a size trigger
+            // or the deadline first.
+            if (opt_.max_delay.count() > 0) {
+                const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
+                while (!full() && more_.wait_until(lk, deadline) != std::cv_status::timeout) {
+                }
             }
             std::vector<Req*> batch;
             std::size_t take = 0, b = 0;
@@ -96,8 +104,16 @@ public:
 
     FrameQueueStats stats() {
         std::lock_guard<std::mutex> lk(mu_);
-        return stats_;
+        FrameQueueStats s = stats_;
+        const std::uint64_t d = direct_.load(std::memory_order_relaxed);
+        s.frames += d;
+        s.flushes += d;
+        s.host_flushes += d;
+        return s;
     }
+    // a frame served on its caller's thread (host engine): one frame, one host pass (an atomic:
+    // a mutex here convoyed 256 session threads on 16 cores down to 158 K frames/s)
+    void count_direct() { direct_.fetch_add(1, std::memory_order_relaxed); }
 
 private:
     bool full() const { return pending_.size() >= opt_.max_frames || bytes_ >= opt_.max_bytes; }
@@ -109,6 +125,7 @@ private:
     std::size_t bytes_ = 0;
     bool busy_ = false;
     FrameQueueStats stats_{};
+    std::atomic<std::uint64_t> direct_{0};
 };
 
 void put_be32(std::uint8_t* p, std::uint32_t v) {
@@ -154,12 +171,57 @@ bool host_wire_open(const std::uint8_t key[32], std::span<const std::uint8_t> f,
     return true;
 }
 
-void draw_nonces(std::random_device& rd, std::vector<Nonce>& nonces) {
-    for (auto& n : nonces)
-        for (int i = 0; i < 12; i += 4) {
-            const std::uint32_t v = rd();
-            std::memcpy(n.bytes.data() + i, &v, 4);
+// Frame nonces.  SessionManager::send draws each nonce from a fresh std::random_device
+// (SessionManager.cpp:365-371); on the box that source serves ~0.4 M nonces/s for the whole
+// machine however many threads ask, which capped every sender.  Each thread here keeps a
+// ChaCha20 keystream generator keyed with 256 bits from std::random_device and re-keyed every
+// 2^20 nonces (the arc4random construction): 12 unpredictable bytes per frame, never reused under
+// one session key.
+class NonceSource {
+public:
+    void draw(Nonce& n) {
+        if (pos_ + 12 > sizeof(buf_)) refill();
+        std::memcpy(n.bytes.data(), buf_ + pos_, 12);
+        std::memset(buf_ + pos_, 0, 12);
+        pos_ += 12;
+    }
+
+private:
+    void refill() {
+        if (left_ == 0) {
+            std::random_device rd;
+            for (int i = 0; i < 32; i += 4) {
+                const std::uint32_t v = rd();
+                std::memcpy(key_ + i, &v, 4);
+            }
+            for (int i = 0; i < 12; i += 4) {
+                const std::uint32_t v = rd();
+                std::memcpy(iv_ + i, &v, 4);
+            }
+            ctr_ = 0;
+            left_ = 1u << 20;
         }
+        std::memset(buf_, 0, sizeof(buf_));
+        enet::host::chacha20_xor(key_, iv_, ctr_, buf_, buf_, sizeof(buf_));
+        ctr_ += sizeof(buf_) / 64;
+        pos_ = 0;
+        const std::uint32_t got = (std::uint32_t)(sizeof(buf_) / 12);
+        left_ = left_ > got ? left_ - got : 0;
+    }
+    std::uint8_t key_[32] = {}, iv_[12] = {};
+    std::uint32_t ctr_ = 0, left_ = 0;
+    std::uint8_t buf_[1020] = {};
+    std::size_t pos_ = sizeof(buf_);
+};
+
+NonceSource& nonce_source() {
+    thread_local NonceSource src;
+    return src;
+}
+
+void draw_nonces(std::vector<Nonce>& nonces) {
+    NonceSource& src = nonce_source();
+    for (auto& n : nonces) src.draw(n);
 }
 
 }  // namespace
@@ -168,8 +230,6 @@ void draw_nonces(std::random_device& rd, std::vector<Nonce>& nonces) {
 struct FrameQueue::Impl {
     explicit Impl(const FrameQueueOptions& o) : flusher(o) {}
     Flusher flusher;
-    std::mutex rd_mu;
-    std::random_device rd;
     // push / flush
     mutable std::mutex manual_mu;
     std::vector<std::array<std::uint8_t, 32>> keys;
@@ -179,10 +239,7 @@ struct FrameQueue::Impl {
     bool seal(std::vector<Req*>& batch) {
         const std::size_t n = batch.size();
         std::vector<Nonce> nonces(n);
-        {
-            std::lock_guard<std::mutex> lk(rd_mu);
-            draw_nonces(rd, nonces);
-        }
+        draw_nonces(nonces);
         if (enet::scalar::g_policy.load() != ENET_SCALAR_HOST) {
             std::vector<std::array<std::uint8_t, 32>> ks(n);
             std::vector<std::span<const std::uint8_t>> ms(n);
@@ -215,6 +272,17 @@ FrameQueue::~FrameQueue() { delete impl_; }
 std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::uint8_t, 32>& session_key,
                                                           std::span<const std::uint8_t> message) {
     if (message.size() + kMac > kMaxPayloadSize) return std::nullopt;  // SessionManager.cpp:358-360
+    if (enet::scalar::g_policy.load() != ENET_SCALAR_DEVICE) {
+        // host engine (policies auto and host): every session thread seals its own frame -- one
+        // MTU frame costs a core ~1 us, a device flush (pageable copies, launch, sync) ~170 us,
+        // so on the box the queue's device pass lost to this at 16 and 256 session threads
+        // (profiles/r03_frame_queue.jsonl); ENET_SCALAR_DEVICE batches on the MI355X
+        Nonce nonce;
+        nonce_source().draw(nonce);
+        enet::scalar::host_call();
+        impl_->flusher.count_direct();
+        return host_wire_seal(session_key.data(), nonce.bytes.data(), message);
+    }
     Req r{session_key.data(), message, {}};
     impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->seal(b); });
     if (!r.ok) return std::nullopt;
@@ -294,6 +362,13 @@ FrameReceiveQueue::~FrameReceiveQueue() { delete impl_; }
 std::optional<std::vector<std::uint8_t>> FrameReceiveQueue::open(const std::array<std::uint8_t, 32>& session_key,
                                                                  std::span<const std::uint8_t> frame) {
     if (!frame_shape_ok(frame)) return std::nullopt;  // never reaches a flush
+    if (enet::scalar::g_policy.load() != ENET_SCALAR_DEVICE) {  // the caller's thread, no queue
+        enet::scalar::host_call();
+        impl_->flusher.count_direct();
+        std::vector<std::uint8_t> m;
+        if (!host_wire_open(session_key.data(), frame, m)) return std::nullopt;
+        return m;
+    }
     Req r{session_key.data(), frame, {}};
     impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->open(b); });
     if (!r.ok) return std::nullopt;

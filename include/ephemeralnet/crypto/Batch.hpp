@@ -81,17 +81,21 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open(
 // Cross-session frame queues.  SessionManager runs one detached reader
 // thread per session (SessionManager.cpp:332-333, receive_loop :703-854) and sends from whatever
 // thread calls Node::send_secure (:337-388).  Instead of one ChaCha20 + HMAC per frame on each of
-// those threads, every thread hands its frame to a shared queue and blocks; the queue flushes
-// when it holds max_frames frames or max_bytes bytes, or max_delay after the first waiting frame,
-// and ONE batched pass (crypto::batch::wire_seal / wire_open on the MI355X) serves everything
-// queued, each caller getting back exactly its own result.  Thread-safe; results are bit-exact
-// with the per-frame reference path.  Routing follows enet_scalar_set_policy: ENET_SCALAR_HOST
-// serves a flush on the host engine, and a failed device flush is finished on the host engine
-// (never an exception into a session thread).
+// those threads, every thread hands its frame to a shared queue and blocks; a waiting thread with
+// no flush in flight takes everything queued (at most max_frames / max_bytes) and runs ONE batched
+// pass (crypto::batch::wire_seal / wire_open on the MI355X), each caller getting back exactly its
+// own result; frames arriving during a pass form the next one (group commit, so batches grow with
+// load).  Thread-safe; results are bit-exact with the per-frame reference path.  Routing follows
+// enet_scalar_set_policy: ENET_SCALAR_DEVICE batches through the queue; ENET_SCALAR_AUTO (the
+// default) and ENET_SCALAR_HOST bypass it -- each thread seals / opens its own frame on the host
+// engine, measured faster than a device pass for MTU frames on the box -- and a
+// failed device flush is finished on the host engine (never an exception into a session thread).
+// Large batches a caller already holds belong on wire_seal / wire_open (the MI355X).
 struct FrameQueueOptions {
-    std::size_t max_frames = 4096;                     // flush at this many queued frames
-    std::size_t max_bytes = 8u << 20;                  // ... or this many queued bytes
-    std::chrono::microseconds max_delay{100};          // ... or this long after a flush could start
+    std::size_t max_frames = 4096;                     // at most this many frames per pass
+    std::size_t max_bytes = 8u << 20;                  // ... and this many bytes
+    std::chrono::microseconds max_delay{0};            // > 0: before a pass, wait this long (or
+                                                       // for a size limit) for more frames
 };
 struct FrameQueueStats {
     std::uint64_t frames = 0;   // frames served
@@ -100,8 +104,9 @@ struct FrameQueueStats {
 };
 
 // Send side: nonce(12) || BE32(|body|) || ChaCha20_{K,nonce,0}(m || HMAC_K(m)), the frame
-// SessionManager::send writes (SessionManager.cpp:362-387).  Nonces: 12 bytes per frame from
-// std::random_device, as SessionManager.cpp:365-371 draws them, taken once per flush.
+// SessionManager::send writes (SessionManager.cpp:362-387).  Nonces: 12 random bytes per frame
+// (the reference draws them from std::random_device, SessionManager.cpp:365-371; here from a
+// per-thread ChaCha20 keystream keyed from std::random_device, re-keyed every 2^20 nonces).
 class ENET_CXX_API FrameQueue {
 public:
     static constexpr std::size_t kMaxPayloadSize = 1024 * 1024;  // SessionManager.cpp:87

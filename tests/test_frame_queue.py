@@ -47,7 +47,6 @@ def check_common(rc, s, sample, threads, frames):
     assert rc == 0 and s["bad"] == 0 and s["wrong"] == 0, s
     assert s["oversize_refused"] == threads
     assert s["tx_frames"] == threads * frames and s["rx_frames"] == s["opened"] + s["rejected"] - 0 or True
-    assert s["tx_flushes"] < s["tx_frames"]  # batched: many frames per flush
     tampered = sum(1 for t in range(threads) for i in range(frames) if i % 7 == 3)
     foreign = sum(1 for t in range(threads) for i in range(frames) if i % 7 != 3 and i % 11 == 4)
     assert s["rejected"] == tampered + foreign
@@ -63,9 +62,11 @@ def check_common(rc, s, sample, threads, frames):
 
 
 def test_queues_16_threads_host_engine(stress_bin):
+    """Host policy: no queue -- every session thread seals / opens its own frame on the host
+    engine (one 'flush' per frame), bit-exact and isolated as through the queue."""
     rc, s, sample, _ = run(stress_bin, "host")
     check_common(rc, s, sample, 16, 150)
-    assert s["tx_host_flushes"] == s["tx_flushes"] and s["device_failures"] == 0
+    assert s["tx_host_flushes"] == s["tx_flushes"] == s["tx_frames"] and s["device_failures"] == 0
 
 
 def test_queues_16_threads_device_failure_on_cpu(stress_bin):
@@ -73,13 +74,28 @@ def test_queues_16_threads_device_failure_on_cpu(stress_bin):
     engine; callers never see an exception or a wrong frame."""
     rc, s, sample, err = run(stress_bin, "device", frames=60)
     check_common(rc, s, sample, 16, 60)
+    assert s["tx_flushes"] < s["tx_frames"]  # batched: many frames per flush
+    if s["device_failures"] == 0 and s["tx_host_flushes"] == 0:
+        pytest.skip("a usable device served every flush (GPU box): covered by the -m gpu tests")
     assert s["device_failures"] >= s["tx_flushes"] > 0
     assert "finished on the host engine" in err
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("policy", ["auto", "device"])
-def test_queues_16_threads_on_gpu(stress_bin, policy):
-    rc, s, sample, err = run(stress_bin, policy)
+def test_queues_16_threads_on_gpu(stress_bin):
+    """Policy device: every flush is one MI355X pass over the frames queued by 16 session
+    threads (batched, no host flush, no device failure), bit-exact and isolated per caller."""
+    rc, s, sample, err = run(stress_bin, "device")
     check_common(rc, s, sample, 16, 150)
+    assert s["tx_flushes"] < s["tx_frames"]  # batched: many frames per flush
     assert s["tx_host_flushes"] == 0 and s["rx_host_flushes"] == 0 and s["device_failures"] == 0, err
+
+
+@pytest.mark.gpu
+def test_queues_16_threads_auto_policy_on_gpu(stress_bin):
+    """Policy auto with a working GPU: the queues route MTU-sized frames to each session thread's
+    host engine (measured faster than a device pass): one host pass per frame,
+    no device failure, same bytes."""
+    rc, s, sample, err = run(stress_bin, "auto")
+    check_common(rc, s, sample, 16, 150)
+    assert s["tx_host_flushes"] == s["tx_flushes"] == s["tx_frames"] and s["device_failures"] == 0, err

@@ -11,7 +11,7 @@
 // Sha256 per attempt).  With ENET_BATCH the drop-in crypto::batch::compute_handshake_pow (one device
 // search) is timed beside it.  Output: one JSON line per case, median and mean microseconds.
 //
-// usage: scalar_latency [reps] [policy auto|device|host (drop-in build only)] [threads]
+// usage: scalar_latency [reps] [policy auto|device|host (drop-in build only)] [threads] [qthreads]
 // After the single-thread latencies, `threads` threads call the same API concurrently for ~1 s
 // per case (the reference's per-session reader threads, SessionManager.cpp:332,703) and the
 // aggregate calls/s and GB/s are printed ("mt_*" cases).
@@ -31,6 +31,8 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <random>
+#include <span>
 #include <atomic>
 #include <string>
 #include <thread>
@@ -188,6 +190,66 @@ int main(int argc, char** argv) {
             ChaCha20::apply(key, nonce, c1m, o, 0); g_sink += o[0]; });
         run_mt("sha256_digest", 65536, threads, 1.0, [&](int, std::vector<std::uint8_t>&) {
             g_sink += Sha256::digest(c64k)[0]; });
+    }
+
+    // Session frames: SessionManager::send seals a 1500-byte message on the
+    // caller's thread as HMAC + ChaCha20 over message || MAC (SessionManager.cpp:362-374,
+    // Message.cpp:305-311), and receive_loop opens it with ChaCha20 + HmacSha256::verify
+    // (:815-822, Message.cpp:313-328); one key per session thread.  Per-call: those reference
+    // calls on every thread (the drop-in build serves them on its host engine).  Queue (drop-in
+    // build): every thread hands its frame to one shared FrameQueue / FrameReceiveQueue, which
+    // seals / opens a whole flush in one MI355X pass (policy device / auto) or on the host engine
+    // (policy host).  `qthreads` session threads (argv[4], default 256: a relay serves hundreds).
+    const int qthreads = argc > 4 ? std::atoi(argv[4]) : 256;
+    for (int nt : {threads, qthreads}) {
+        if (nt <= 0) continue;
+        std::vector<Key> keys(nt);
+        for (int t = 0; t < nt; ++t)
+            for (int i = 0; i < 32; ++i) keys[t].bytes[i] = static_cast<std::uint8_t>(i * 7 + t);
+        // as SessionManager::send is written: a fresh std::random_device per frame, one draw per
+        // nonce byte (:365-371), then HMAC and ChaCha20 over message || MAC
+        run_mt("frame_seal_percall", 1500, nt, 1.0, [&](int t, std::vector<std::uint8_t>& o) {
+            Nonce fn{};
+            {
+                std::random_device rd;
+                for (auto& b : fn.bytes) b = static_cast<std::uint8_t>(rd());
+            }
+            g_sink += fn.bytes[0];
+            const auto m = HmacSha256::compute(keys[t].bytes, f1500);
+            std::vector<std::uint8_t> sig(f1500);
+            sig.insert(sig.end(), m.begin(), m.end());
+            ChaCha20::apply(keys[t], fn, sig, o, 0);
+            g_sink += o[0]; });
+        std::vector<std::vector<std::uint8_t>> bodies(nt);
+        for (int t = 0; t < nt; ++t) {
+            const auto m = HmacSha256::compute(keys[t].bytes, f1500);
+            std::vector<std::uint8_t> sig(f1500);
+            sig.insert(sig.end(), m.begin(), m.end());
+            ChaCha20::apply(keys[t], nonce, sig, bodies[t], 0);
+        }
+        run_mt("frame_open_percall", 1500, nt, 1.0, [&](int t, std::vector<std::uint8_t>& o) {
+            ChaCha20::apply(keys[t], nonce, bodies[t], o, 0);
+            const std::span<const std::uint8_t> msg(o.data(), o.size() - 32), tag(o.data() + o.size() - 32, 32);
+            g_sink += HmacSha256::verify(keys[t].bytes, msg, tag); });
+#ifdef ENET_BATCH
+        batch::FrameQueue tx;
+        batch::FrameReceiveQueue rx;
+        std::vector<std::array<std::uint8_t, 32>> sk(nt);
+        for (int t = 0; t < nt; ++t) std::copy(keys[t].bytes.begin(), keys[t].bytes.end(), sk[t].begin());
+        run_mt("frame_queue_seal", 1500, nt, 1.5, [&](int t, std::vector<std::uint8_t>&) {
+            g_sink += tx.seal(sk[t], f1500)->size(); });
+        std::vector<std::vector<std::uint8_t>> wire(nt);
+        for (int t = 0; t < nt; ++t) wire[t] = *tx.seal(sk[t], f1500);
+        run_mt("frame_queue_open", 1500, nt, 1.5, [&](int t, std::vector<std::uint8_t>&) {
+            g_sink += rx.open(sk[t], wire[t])->size(); });
+        const auto ts = tx.stats(), rs = rx.stats();
+        std::printf("{\"case\": \"frame_queue_stats\", \"threads\": %d, \"tx_frames\": %llu, \"tx_flushes\": %llu, "
+                    "\"tx_host_flushes\": %llu, \"rx_frames\": %llu, \"rx_flushes\": %llu, \"rx_host_flushes\": %llu}\n",
+                    nt, (unsigned long long)ts.frames, (unsigned long long)ts.flushes,
+                    (unsigned long long)ts.host_flushes, (unsigned long long)rs.frames,
+                    (unsigned long long)rs.flushes, (unsigned long long)rs.host_flushes);
+        std::fflush(stdout);
+#endif
     }
 
     // handshake PoW at difficulty 8 (about 256 attempts expected), 5 different peers
