@@ -201,16 +201,19 @@ private:
             ctr_ = 0;
             left_ = 1u << 20;
         }
+        // whole keystream blocks only: the next refill starts at the next unused block, so no
+        // keystream byte (and no nonce) is ever handed out twice
         std::memset(buf_, 0, sizeof(buf_));
         enet::host::chacha20_xor(key_, iv_, ctr_, buf_, buf_, sizeof(buf_));
-        ctr_ += sizeof(buf_) / 64;
+        ctr_ += kBlocks;
         pos_ = 0;
-        const std::uint32_t got = (std::uint32_t)(sizeof(buf_) / 12);
-        left_ = left_ > got ? left_ - got : 0;
+        left_ = left_ > kPerFill ? left_ - kPerFill : 0;
     }
+    static constexpr std::uint32_t kBlocks = 16;                      // keystream blocks per fill
+    static constexpr std::uint32_t kPerFill = kBlocks * 64 / 12;     // 85 nonces per fill
     std::uint8_t key_[32] = {}, iv_[12] = {};
     std::uint32_t ctr_ = 0, left_ = 0;
-    std::uint8_t buf_[1020] = {};
+    std::uint8_t buf_[kBlocks * 64] = {};
     std::size_t pos_ = sizeof(buf_);
 };
 

@@ -2,6 +2,8 @@
 // (crypto::batch::FrameQueue / FrameReceiveQueue).
 //
 // usage: queue_stress <policy auto|device|host> <threads> <frames per thread> <seed>
+//        queue_stress nonces <policy> <threads> <frames per thread>: every thread seals that many
+//        empty messages under ONE shared key; prints how many of the nonces were distinct
 // Phase 1: every thread seals its own session's messages (lengths 0..3000, some 64 KiB, one
 // frame of the 1 MiB maximum payload per run) through ONE shared FrameQueue.  Phase 2: every
 // thread opens its own frames through ONE shared FrameReceiveQueue, with every 7th frame
@@ -9,6 +11,7 @@
 // session key.  Each thread checks that exactly the untouched frames come back, byte-equal to its
 // own messages.  Prints a sample of (key, message, frame) lines for the oracle check in
 // tests/test_frame_queue.py and a summary line.
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -43,7 +46,37 @@ std::string hex(const std::vector<std::uint8_t>& v) {
 
 }  // namespace
 
+int nonce_uniqueness(const std::string& policy, int T, int F) {
+    enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
+                                                                                      : ENET_SCALAR_AUTO, 0);
+    FrameQueue tx;
+    std::array<std::uint8_t, 32> key{};
+    key[0] = 1;
+    std::vector<std::vector<std::array<std::uint8_t, 12>>> got(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            got[t].reserve(F);
+            for (int i = 0; i < F; ++i) {
+                const auto f = tx.seal(key, {});
+                std::array<std::uint8_t, 12> n{};
+                std::copy(f->begin(), f->begin() + 12, n.begin());
+                got[t].push_back(n);
+            }
+        });
+    for (auto& x : th) x.join();
+    std::vector<std::array<std::uint8_t, 12>> all;
+    for (auto& g : got) all.insert(all.end(), g.begin(), g.end());
+    std::sort(all.begin(), all.end());
+    const auto distinct = std::unique(all.begin(), all.end()) - all.begin();
+    std::printf("nonces total=%zu distinct=%td\n", all.size(), distinct);
+    return distinct == (std::ptrdiff_t)all.size() ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "nonces")
+        return nonce_uniqueness(argc > 2 ? argv[2] : "auto", argc > 3 ? std::atoi(argv[3]) : 8,
+                                argc > 4 ? std::atoi(argv[4]) : 10000);
     const std::string policy = argc > 1 ? argv[1] : "auto";
     const int T = argc > 2 ? std::atoi(argv[2]) : 16;
     const int F = argc > 3 ? std::atoi(argv[3]) : 200;

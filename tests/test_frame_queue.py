@@ -61,6 +61,19 @@ def check_common(rc, s, sample, threads, frames):
     assert len({bytes.fromhex(f)[:12] for _, _, f in sample}) == len(sample)  # fresh nonces
 
 
+@pytest.mark.parametrize("policy", ["host", "device"])
+def test_frame_nonces_never_repeat(stress_bin, policy):
+    """8 threads x 30 000 frames under ONE session key: every nonce distinct (each thread's
+    ChaCha20 nonce generator hands out whole keystream blocks once; refills and re-keys included).
+    CPU: host engine (device policy finishes its flushes on the host with no device)."""
+    if policy == "device" and os.path.exists("/dev/kfd"):
+        pytest.skip("device flushes are covered by the -m gpu queue tests")
+    r = subprocess.run([stress_bin, "nonces", policy, "8", "30000"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, (r.stdout[-500:], r.stderr[-500:])
+    assert "total=240000 distinct=240000" in r.stdout
+
+
 def test_queues_16_threads_host_engine(stress_bin):
     """Host policy: no queue -- every session thread seals / opens its own frame on the host
     engine (one 'flush' per frame), bit-exact and isolated as through the queue."""
