@@ -1,11 +1,10 @@
 // frame_queue.cpp -- the cross-session frame queues of Batch.hpp.
 //
-// Many session threads each submit one frame and block.  Whichever waiting thread finds no flush
-// in flight becomes the leader: it takes what is queued (up to max_frames / max_bytes; with a
-// positive max_delay it first waits for a size trigger or the deadline), runs ONE batched pass --
-// crypto::batch::wire_seal / wire_open on the MI355X -- writes every caller's result into that
-// caller's request and wakes them all; frames arriving meanwhile form the next batch (group
-// commit).  Under the auto and host policies there is no queue: each thread seals / opens its own
+// Many session threads each submit one frame and block.  The queue's worker thread takes what is
+// queued (up to max_frames / max_bytes; with a positive max_delay it first waits for a size limit
+// or the deadline), runs ONE batched pass -- crypto::batch::wire_seal / wire_open on the MI355X --
+// writes every caller's result into that caller's request and wakes exactly those callers;
+// frames arriving meanwhile form the next batch (group commit).  Under the auto and host policies there is no queue: each thread seals / opens its own
 // frame on the host engine, which measured faster than a device pass for MTU frames (see seal()).  A request is owned by the thread that
 // submitted it (it lives on that thread's stack until `done`), results are matched by request,
 // never by position in some shared buffer, so sessions cannot see each other's frames.
@@ -15,8 +14,11 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstring>
 #include <mutex>
+#include <new>
 #include <random>
 #include <vector>
 
@@ -38,68 +40,37 @@ struct Req {
     std::vector<std::uint8_t> out;     // frame (send) or message (receive)
     bool ok = false;
     bool done = false;
+    std::condition_variable cv;        // wakes exactly this waiter
 };
 
-// The leader protocol shared by both directions; Exec(std::vector<Req*>&) fills out / ok.
+// The batching shared by both directions: one worker thread per queue runs every device pass
+// (started on first use), so the pass's staging buffers and HIP stream are allocated once -- with
+// the lead rotating over the callers, each of 256 session threads paid its own first-use
+// allocations (~1.5 ms per pass at 78 frames).  Callers sleep on their own condition variable and
+// are woken exactly when the pass carrying their frame is done; frames arriving during a pass form
+// the next one (group commit).
 class Flusher {
 public:
-    explicit Flusher(const FrameQueueOptions& o) : opt_(o) {
+    using Exec = std::function<bool(std::vector<Req*>&)>;  // fills out / ok; true = host engine
+    Flusher(const FrameQueueOptions& o, Exec exec) : opt_(o), exec_(std::move(exec)) {
         opt_.max_frames = std::max<std::size_t>(1, opt_.max_frames);
     }
+    ~Flusher() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        work_.notify_one();
+        if (worker_.joinable()) worker_.join();
+    }
 
-    template <class Exec>
-    void submit(Req& r, Exec&& exec) {
+    void submit(Req& r) {
         std::unique_lock<std::mutex> lk(mu_);
+        if (!worker_.joinable()) worker_ = std::thread([this] { run(); });
         pending_.push_back(&r);
         bytes_ += r.in.size();
-        if (full()) more_.notify_one();
-        while (!r.done) {
-            if (busy_) {
-                done_.wait(lk);
-                continue;
-            }
-            busy_ = true;
-            // group commit: frames that arrive while a flush runs queue up for the next leader, so
-            // under load the batch grows with the flush time and no deadline is needed (max_delay
-            // 0, the default).  A positive max_delay makes the leader also wait for a size trigger
-            // or the deadline first.
-            if (opt_.max_delay.count() > 0) {
-                const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
-                while (!full() && more_.wait_until(lk, deadline) != std::cv_status::timeout) {
-                }
-            }
-            std::vector<Req*> batch;
-            std::size_t take = 0, b = 0;
-            while (take < pending_.size() && take < opt_.max_frames &&
-                   (take == 0 || b + pending_[take]->in.size() <= opt_.max_bytes)) {
-                b += pending_[take]->in.size();
-                ++take;
-            }
-            batch.assign(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
-            pending_.erase(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
-            bytes_ -= b;
-            lk.unlock();
-            bool host = false;
-            try {
-                host = exec(batch);
-            } catch (...) {  // only std::bad_alloc gets here: fail the batch, keep the queue alive
-                lk.lock();
-                for (Req* q : batch) {
-                    q->ok = false;
-                    q->done = true;
-                }
-                busy_ = false;
-                done_.notify_all();
-                throw;
-            }
-            lk.lock();
-            for (Req* q : batch) q->done = true;
-            stats_.frames += batch.size();
-            stats_.flushes += 1;
-            stats_.host_flushes += host ? 1 : 0;
-            busy_ = false;
-            done_.notify_all();
-        }
+        work_.notify_one();
+        r.cv.wait(lk, [&] { return r.done; });
     }
 
     FrameQueueStats stats() {
@@ -118,14 +89,58 @@ public:
 private:
     bool full() const { return pending_.size() >= opt_.max_frames || bytes_ >= opt_.max_bytes; }
 
+    void run() {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            work_.wait(lk, [&] { return stop_ || !pending_.empty(); });
+            if (pending_.empty()) return;  // stop_ with nothing queued
+            // no deadline by default (max_delay 0): the batch is whatever queued up during the
+            // previous pass; a positive max_delay also waits for a size limit or the deadline
+            if (opt_.max_delay.count() > 0) {
+                const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
+                work_.wait_until(lk, deadline, [&] { return stop_ || full(); });
+            }
+            std::vector<Req*> batch;
+            std::size_t take = 0, b = 0;
+            while (take < pending_.size() && take < opt_.max_frames &&
+                   (take == 0 || b + pending_[take]->in.size() <= opt_.max_bytes)) {
+                b += pending_[take]->in.size();
+                ++take;
+            }
+            batch.assign(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
+            pending_.erase(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
+            bytes_ -= b;
+            lk.unlock();
+            bool host = false, failed = false;
+            try {
+                host = exec_(batch);
+            } catch (...) {  // only std::bad_alloc gets here: fail the batch, keep the queue alive
+                failed = true;
+            }
+            lk.lock();
+            for (Req* q : batch) {
+                if (failed) q->ok = false;
+                q->done = true;
+                q->cv.notify_one();
+            }
+            if (!failed) {
+                stats_.frames += batch.size();
+                stats_.flushes += 1;
+                stats_.host_flushes += host ? 1 : 0;
+            }
+        }
+    }
+
     FrameQueueOptions opt_;
+    Exec exec_;
     std::mutex mu_;
-    std::condition_variable more_, done_;
+    std::condition_variable work_;
     std::vector<Req*> pending_;
     std::size_t bytes_ = 0;
-    bool busy_ = false;
+    bool stop_ = false;
     FrameQueueStats stats_{};
     std::atomic<std::uint64_t> direct_{0};
+    std::thread worker_;
 };
 
 void put_be32(std::uint8_t* p, std::uint32_t v) {
@@ -231,7 +246,7 @@ void draw_nonces(std::vector<Nonce>& nonces) {
 
 // ------------------------------------------------------------------------------ send
 struct FrameQueue::Impl {
-    explicit Impl(const FrameQueueOptions& o) : flusher(o) {}
+    explicit Impl(const FrameQueueOptions& o) : flusher(o, [this](std::vector<Req*>& b) { return seal(b); }) {}
     Flusher flusher;
     // push / flush
     mutable std::mutex manual_mu;
@@ -287,7 +302,7 @@ std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::
         return host_wire_seal(session_key.data(), nonce.bytes.data(), message);
     }
     Req r{session_key.data(), message, {}};
-    impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->seal(b); });
+    impl_->flusher.submit(r);
     if (!r.ok) return std::nullopt;
     return std::move(r.out);
 }
@@ -330,7 +345,7 @@ FrameQueueStats FrameQueue::stats() const { return impl_->flusher.stats(); }
 
 // ------------------------------------------------------------------------------ receive
 struct FrameReceiveQueue::Impl {
-    explicit Impl(const FrameQueueOptions& o) : flusher(o) {}
+    explicit Impl(const FrameQueueOptions& o) : flusher(o, [this](std::vector<Req*>& b) { return open(b); }) {}
     Flusher flusher;
 
     bool open(std::vector<Req*>& batch) {
@@ -373,7 +388,7 @@ std::optional<std::vector<std::uint8_t>> FrameReceiveQueue::open(const std::arra
         return m;
     }
     Req r{session_key.data(), frame, {}};
-    impl_->flusher.submit(r, [&](std::vector<Req*>& b) { return impl_->open(b); });
+    impl_->flusher.submit(r);
     if (!r.ok) return std::nullopt;
     return std::move(r.out);
 }
