@@ -20,6 +20,7 @@
 #include <mutex>
 #include <new>
 #include <random>
+#include <system_error>
 #include <vector>
 
 #include "enet_crypto.h"
@@ -66,7 +67,21 @@ public:
 
     void submit(Req& r) {
         std::unique_lock<std::mutex> lk(mu_);
-        if (!worker_.joinable()) worker_ = std::thread([this] { run(); });
+        if (!worker_.joinable()) {
+            try {
+                worker_ = std::thread([this] { run(); });
+            } catch (const std::system_error&) {  // no thread to be had: serve this frame here
+                lk.unlock();
+                std::vector<Req*> one{&r};
+                const bool host = exec_(one);
+                lk.lock();
+                r.done = true;
+                stats_.frames += 1;
+                stats_.flushes += 1;
+                stats_.host_flushes += host ? 1 : 0;
+                return;
+            }
+        }
         pending_.push_back(&r);
         bytes_ += r.in.size();
         work_.notify_one();
