@@ -93,6 +93,10 @@ def parse():
                          "0 = handshake PoW (start + attempt, 88-byte prefix)")
     ap.add_argument("--prewarm-s", type=float, default=0.3,
                     help="untimed clock-ramp seal/open pairs before the warmup steps (seconds, 0 = off)")
+    ap.add_argument("--sessions", type=int, default=0,
+                    help="--mode wire: frames filed round-robin under this many session keys (a key "
+                         "table + HMAC midstates computed inside every step, "
+                         "enet_wire_*_batch_sessions); 0 = a key per frame")
     ap.add_argument("--store-ids", default="given", choices=["given", "content"],
                     help="store mode: caller-given chunk ids (fused kernel) or content-derived")
     ap.add_argument("--mode", default="aead", choices=["aead", "xor", "wire", "store", "pow"],
@@ -711,6 +715,15 @@ def main():
         frames = torch.empty(n * F, dtype=torch.uint8, device=dev)
         macs = torch.empty(32 * n, dtype=torch.uint8, device=dev)
         wire_b = E.Batch(frames, foffs, keys, None, total_bytes_hint=n * F, max_len_hint=F)
+        if args.sessions:
+            K = args.sessions
+            if not 0 < K <= n:
+                raise SystemExit("--sessions must be in [1, records]")
+            sess_tbl = keys[:32 * K]  # session key table; frame i belongs to session i mod K
+            sess_idx = (torch.arange(n, dtype=torch.int32, device=dev) % K).contiguous()
+            sess_mid = torch.empty(16 * K, dtype=torch.int32, device=dev)
+            seal_b = E.Batch(pt, offs, sess_tbl, nonces, total_bytes_hint=n * L, max_len_hint=L)
+            wire_b = E.Batch(frames, foffs, sess_tbl, None, total_bytes_hint=n * F, max_len_hint=F)
     if args.mode == "store":
         hashes = torch.empty(32 * n, dtype=torch.uint8, device=dev)
         # Node::store_chunk(chunk_id, data) takes the id from its caller (ControlServer.cpp:1101
@@ -722,6 +735,9 @@ def main():
     def seal():
         if args.mode == "aead":
             E.aead_seal(seal_b, ct, tags, stream=stream)
+        elif args.mode == "wire" and args.sessions:
+            E.hmac_midstates(sess_tbl, args.sessions, sess_mid, stream=stream)
+            E.wire_seal_sessions(seal_b, frames, foffs, sess_idx, args.sessions, sess_mid, stream=stream)
         elif args.mode == "wire":
             E.wire_seal(seal_b, frames, foffs, stream=stream)
         elif args.mode == "store":
@@ -732,6 +748,8 @@ def main():
     def open_():
         if args.mode == "aead":
             E.aead_open(open_b, back, tags, ok, stream=stream)
+        elif args.mode == "wire" and args.sessions:
+            E.wire_open_sessions(wire_b, back, offs, sess_idx, args.sessions, sess_mid, macs, ok, stream=stream)
         elif args.mode == "wire":
             E.wire_open(wire_b, back, offs, macs, ok, stream=stream)
         elif args.mode == "store":
@@ -882,8 +900,10 @@ def main():
             "dtype": "u32",
             "data": "synthetic (torch.randint on device; random per-record keys and nonces)",
             "config": {
-                "workload": f"{WORKLOADS.get((n, L), 'custom')}: {n} x {L} B records, per-record "
-                            f"(key, nonce), {MODE_DESC[args.mode]}, device-resident",
+                "workload": f"{WORKLOADS.get((n, L), 'custom')}: {n} x {L} B records, "
+                            + (f"{args.sessions} session keys (round-robin), per-record nonce"
+                               if args.mode == "wire" and args.sessions else "per-record (key, nonce)")
+                            + f", {MODE_DESC[args.mode]}, device-resident",
                 "records_per_gpu": n,
                 "record_bytes": L,
                 "lanes_per_record": E.lanes_per_record(n, n * L, L),

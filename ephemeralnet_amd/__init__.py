@@ -53,7 +53,8 @@ EXPORTS = [
     "enet_chacha20_xor_batch", "enet_aead_seal_batch", "enet_aead_open_batch",
     "enet_sha256_batch", "enet_hmac_sha256_batch", "enet_hmac_sha256_verify_batch",
     "enet_frame_seal_batch", "enet_frame_open_batch", "enet_wire_seal_batch",
-    "enet_wire_open_batch", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
+    "enet_wire_open_batch", "enet_hmac_midstates", "enet_wire_seal_batch_sessions",
+    "enet_wire_open_batch_sessions", "enet_chunk_store_batch", "enet_chunk_fetch_batch",
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split",
@@ -93,6 +94,9 @@ def lib() -> C.CDLL:
         L.enet_frame_open_batch.argtypes = [rp, vp, vp, vp]
         L.enet_wire_seal_batch.argtypes = [rp, vp]
         L.enet_wire_open_batch.argtypes = [rp, vp, vp, vp]
+        L.enet_hmac_midstates.argtypes = [vp, u32, vp, vp]
+        L.enet_wire_seal_batch_sessions.argtypes = [rp, vp, u32, vp, vp]
+        L.enet_wire_open_batch_sessions.argtypes = [rp, vp, u32, vp, vp, vp, vp]
         L.enet_chunk_store_batch.argtypes = [rp, vp, vp, vp]
         L.enet_chunk_fetch_batch.argtypes = [rp, vp, vp, vp, vp]
         L.enet_aead_hmac_seal_batch.argtypes = [rp, vp, vp, vp]
@@ -267,6 +271,27 @@ def wire_open(b: Batch, out, out_offsets, macs, ok, stream=None) -> None:
     r = b.records(out, out_offsets)
     _check(lib().enet_wire_open_batch(C.byref(r), _ptr(macs), _ptr(ok), _stream(stream)),
            "enet_wire_open_batch")
+
+
+def hmac_midstates(keys, n: int, mid, stream=None) -> None:
+    """mid[16 i .. 16 i + 16) = HMAC-SHA256 ipad / opad midstates of the 32-byte key i."""
+    _check(lib().enet_hmac_midstates(_ptr(keys), n, _ptr(mid), _stream(stream)), "enet_hmac_midstates")
+
+
+def wire_seal_sessions(b: Batch, out, out_offsets, session, sessions: int, mid, stream=None) -> None:
+    """wire_seal with b.keys a table of `sessions` keys, session[i] (int32) the session of frame i
+    and mid the table's hmac_midstates (same bytes as wire_seal with per-frame keys
+    table[session[i]]; an index >= sessions seals that frame with a zero MAC)."""
+    r = b.records(out, out_offsets)
+    _check(lib().enet_wire_seal_batch_sessions(C.byref(r), _ptr(session), sessions, _ptr(mid),
+                                               _stream(stream)), "enet_wire_seal_batch_sessions")
+
+
+def wire_open_sessions(b: Batch, out, out_offsets, session, sessions: int, mid, macs, ok, stream=None) -> None:
+    """wire_open under a session-key table (see wire_seal_sessions); ok[i] = 0 for an index >= sessions."""
+    r = b.records(out, out_offsets)
+    _check(lib().enet_wire_open_batch_sessions(C.byref(r), _ptr(session), sessions, _ptr(mid), _ptr(macs),
+                                               _ptr(ok), _stream(stream)), "enet_wire_open_batch_sessions")
 
 
 def chunk_store(b: Batch, out, chunk_hashes, chunk_ids=None, stream=None) -> None:

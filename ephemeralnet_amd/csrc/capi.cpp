@@ -537,6 +537,46 @@ int enet_wire_seal_batch(const enet_records* r, void* stream) {
     return hip_status(enet::launch_records(3, p, lanes_for(r), st), "wire_seal chacha launch");
 }
 
+int enet_hmac_midstates(const uint8_t* keys, uint32_t n, uint32_t* mid, void* stream) {
+    if (n == 0) return ENET_OK;
+    if (!keys || !mid || !aligned4(keys) || !aligned4(mid)) return fail(ENET_EINVAL, "hmac_midstates: NULL/misaligned keys or mid");
+    return hip_status(enet::launch_hmac_midstates(n, keys, mid, (hipStream_t)stream), "hmac_midstates");
+}
+
+// the session-keyed frame paths always run the one-pass duplex kernel
+int enet_wire_seal_batch_sessions(const enet_records* r, const uint32_t* session, uint32_t sessions,
+                                  const uint32_t* mid, void* stream) {
+    if (int e = check_records(r, true)) return e;
+    if (r->count == 0) return ENET_OK;
+    if (!session || !mid || !aligned4(session) || !aligned4(mid) || sessions == 0) return fail(ENET_EINVAL, "wire_seal_sessions: NULL/misaligned session or mid, or no sessions");
+    enet::DuplexParams d = duplex_params(r);
+    d.hdr = kWireHeader;
+    d.session = session;
+    d.mid = mid;
+    d.n_sessions = sessions;
+    return hip_status(enet::launch_duplex(enet::DK_FRAME, false, d, (hipStream_t)stream), "wire_seal_sessions");
+}
+
+int enet_wire_open_batch_sessions(const enet_records* r, const uint32_t* session, uint32_t sessions,
+                                  const uint32_t* mid, uint8_t* macs, uint8_t* ok, void* stream) {
+    if (!r) return fail(ENET_EINVAL, "records descriptor is NULL");
+    if (r->count == 0) return ENET_OK;
+    enet_records q = *r;
+    static const uint32_t kNoNonce[3] = {0, 0, 0};
+    if (!q.nonces) q.nonces = reinterpret_cast<const uint8_t*>(kNoNonce);  // read from frames
+    if (int e = check_records(&q, true)) return e;
+    if (!macs || !ok || !aligned4(macs)) return fail(ENET_EINVAL, "wire_open_sessions: NULL/misaligned macs or NULL ok");
+    if (!session || !mid || !aligned4(session) || !aligned4(mid) || sessions == 0) return fail(ENET_EINVAL, "wire_open_sessions: NULL/misaligned session or mid, or no sessions");
+    enet::DuplexParams d = duplex_params(&q);
+    d.hdr = kWireHeader;
+    d.macs = macs;
+    d.ok = ok;
+    d.session = session;
+    d.mid = mid;
+    d.n_sessions = sessions;
+    return hip_status(enet::launch_duplex(enet::DK_FRAME, true, d, (hipStream_t)stream), "wire_open_sessions");
+}
+
 int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream) {
     if (!r) return fail(ENET_EINVAL, "records descriptor is NULL");
     if (r->count == 0) return ENET_OK;

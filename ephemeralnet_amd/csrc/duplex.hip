@@ -153,9 +153,14 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         return *reinterpret_cast<const uint4*>(d);
     };
 
+    // session-keyed frames: an index outside the table reads session 0 and the frame fails (a
+    // zero MAC on seal, ok = 0 on open) instead of reading past the table
+    const uint32_t sraw = (p.session && live) ? p.session[rec] : 0u;
+    const bool sbad = p.session && sraw >= p.n_sessions;
+    const uint32_t sid = sbad ? 0u : sraw;
     uint32_t kw[8];
     {
-        const uint8_t* kp = p.keys + (size_t)p.key_stride * rec;
+        const uint8_t* kp = p.session ? p.keys + 32ull * sid : p.keys + (size_t)p.key_stride * rec;
 #pragma unroll
         for (int i = 0; i < 8; ++i) kw[i] = live ? reinterpret_cast<const uint32_t*>(kp)[i] : 0u;
     }
@@ -333,12 +338,19 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) kb[i] = bswap32(kw[i]);
         uint32_t st[8], x[16];
+        // session-keyed frames: the session's midstates replace the ipad / opad compressions
+        const uint32_t* ms = (KIND == DK_FRAME && p.mid && live) ? p.mid + 16ull * sid : nullptr;
 #pragma unroll
         for (int i = 0; i < 8; ++i) st[i] = kShaIV[i];
         if (KIND != DK_CHUNK) {
+            if (ms) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x36363636u;
-            sha256_compress(st, x);
+                for (int i = 0; i < 8; ++i) st[i] = ms[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x36363636u;
+                sha256_compress(st, x);
+            }
         }
         for (uint32_t s = 0; s < Tmax; ++s) {
             ENET_DX_BARRIER();
@@ -389,11 +401,16 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 uint32_t inner[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) inner[i] = st[i];
+                if (ms) {
 #pragma unroll
-                for (int i = 0; i < 8; ++i) st[i] = kShaIV[i];
+                    for (int i = 0; i < 8; ++i) st[i] = ms[8 + i];
+                } else {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x5c5c5c5cu;
-                sha256_compress(st, x);
+                    for (int i = 0; i < 8; ++i) st[i] = kShaIV[i];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) x[i] = (i < 8 ? kb[i] : 0u) ^ 0x5c5c5c5cu;
+                    sha256_compress(st, x);
+                }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) x[i] = inner[i];
                 x[8] = 0x80000000u;
@@ -403,7 +420,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 sha256_compress(st, x);
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = bswap32(st[i]);
+            for (int i = 0; i < 8; ++i) d[i] = sbad ? 0u : bswap32(st[i]);
         }
         if (!OPEN) {
             if (valid) {
@@ -419,7 +436,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
             }
             ENET_DX_BARRIER();  // T2
         } else if (live) {
-            uint32_t diff = valid ? 0u : 1u;
+            uint32_t diff = (valid && !sbad) ? 0u : 1u;
             if (valid) {
                 if (KIND == DK_FRAME) {  // HmacSha256::verify (HmacSha256.cpp:41-54)
                     uint32_t e[8];

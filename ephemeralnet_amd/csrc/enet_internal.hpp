@@ -115,6 +115,12 @@ struct DuplexParams {
     uint32_t max_len;          // host hint: longest record (scheduling only; 0 = unknown)
     int prio;                  // issue priority: 0 = length-graded (default), -1 = none,
                                // 1 = hash waves first, 2 = cipher waves first
+    // session-keyed frames (nullable): record i uses key keys[32 * session[i]] and the session's
+    // HMAC midstates mid[16 * session[i]] (inner state, outer state) instead of absorbing
+    // key ^ ipad / key ^ opad itself
+    const uint32_t* session;
+    const uint32_t* mid;
+    uint32_t n_sessions;  // session[i] >= n_sessions: the frame never authenticates
 };
 hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t s);
 // chunk / AEAD+HMAC kinds with each record's work split over cipher, schedule and rounds waves
@@ -139,6 +145,10 @@ struct PowParams {
 };
 hipError_t launch_pow_search(const PowParams& p, uint32_t waves, hipStream_t s);
 hipError_t launch_pow_check(const PowParams& p, hipStream_t s);
+
+// HMAC-SHA256 midstates of n 32-byte keys: mid[16 i .. 16 i + 8) = state after (key ^ ipad),
+// mid[16 i + 8 .. 16 i + 16) = state after (key ^ opad) (sha.hip)
+hipError_t launch_hmac_midstates(uint32_t n, const uint8_t* keys, uint32_t* mid, hipStream_t s);
 
 // KeyManager::derive_key for many sessions (sha.hip)
 hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,

@@ -213,6 +213,37 @@ __global__ __launch_bounds__(kWG) void session_key_kernel(uint32_t n, const uint
     o[1] = make_uint4(bswap32(st[4]), bswap32(st[5]), bswap32(st[6]), bswap32(st[7]));
 }
 
+// HMAC-SHA256 midstates of a session-key table (HmacSha256.cpp:11-39 with 32-byte keys: the key
+// block is key || 0^32): the states after absorbing key ^ ipad and key ^ opad, one key per lane.
+// Frames of one session then start their inner and outer hashes from these (duplex.hip).
+__global__ __launch_bounds__(kWG) void hmac_midstate_kernel(uint32_t n, const uint8_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ mid) {
+    const uint32_t i = blockIdx.x * kWG + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* kp = reinterpret_cast<const uint32_t*>(keys + 32ull * i);
+    uint32_t kb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kb[j] = bswap32(kp[j]);
+    uint32_t* o = mid + 16ull * i;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t pad = pass == 0 ? 0x36363636u : 0x5c5c5c5cu;
+        uint32_t st[8], w[16];
+        sha_init(st);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = (j < 8 ? kb[j] : 0u) ^ pad;
+        sha256_compress(st, w);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[8 * pass + j] = st[j];
+    }
+}
+
+hipError_t launch_hmac_midstates(uint32_t n, const uint8_t* keys, uint32_t* mid, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(hmac_midstate_kernel, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s, n, keys, mid);
+    return hipGetLastError();
+}
+
 hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
                                const int64_t* ticks, uint8_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;

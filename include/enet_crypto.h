@@ -127,6 +127,21 @@ ENET_API int enet_frame_open_batch(const enet_records* r, uint8_t* macs, uint8_t
  *       length; failed messages are zeroed. */
 ENET_API int enet_wire_seal_batch(const enet_records* r, void* stream);
 ENET_API int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t* ok, void* stream);
+/* Session-keyed frame batches (a relay's frames come from fewer sessions than
+ * frames).  keys = the sessions' 32-byte keys as a table ([sessions][32], key_stride ignored),
+ * session[i] = the session of frame i, mid = the table's HMAC midstates from
+ * enet_hmac_midstates ([sessions][16] uint32).  Same bytes as enet_wire_seal_batch /
+ * enet_wire_open_batch with keys[i] = table[session[i]]; every frame skips the two key-block
+ * compressions of its HMAC (2 of 27 for a 1 500-byte message).  A session[i] >= sessions
+ * (device-resident, so not checked on the host) never reads past the table: seal writes that
+ * frame with an all-zero MAC (it never authenticates), open reports ok[i] = 0.  enet_hmac_midstates: for each of
+ * n keys the SHA-256 states after (key || 0^32) ^ ipad and ^ opad (HmacSha256.cpp:11-39). */
+ENET_API int enet_hmac_midstates(const uint8_t* keys, uint32_t n, uint32_t* mid, void* stream);
+ENET_API int enet_wire_seal_batch_sessions(const enet_records* r, const uint32_t* session,
+                                           uint32_t sessions, const uint32_t* mid, void* stream);
+ENET_API int enet_wire_open_batch_sessions(const enet_records* r, const uint32_t* session,
+                                           uint32_t sessions, const uint32_t* mid, uint8_t* macs,
+                                           uint8_t* ok, void* stream);
 
 /* ---- AEAD with a fused HMAC-SHA256 integrity tag ("AEAD plus fused
  *      HMAC-SHA256 tag and verify"): ONE pass over HBM per direction (duplex kernel: Poly1305

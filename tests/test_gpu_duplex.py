@@ -472,3 +472,56 @@ def test_split_kernel_edge_lengths_vs_oracle(enet, kind, base):
                 assert seg[i] == c, i
     finally:
         enet.set_duplex_split(-1)
+
+
+def test_wire_frames_sessions_vs_per_frame_keys(enet):
+    """Session-keyed wire frames (enet_wire_seal/open_batch_sessions): a table
+    of 37 session keys, frames filed under sessions at random, the sessions' HMAC midstates
+    computed once (enet_hmac_midstates) instead of the two key-block compressions per frame.
+    Bit-exact with the per-frame-key path (keys[i] = table[session[i]]) and with the oracle's
+    SessionManager::send restatement; opening accepts every frame, rejects a tampered body, a
+    frame filed under another session and session indices past the table (seal: zero MAC, open:
+    ok = 0 -- never a read past the table), and zeroes their plaintext."""
+    import torch
+    rng = np.random.default_rng(9)
+    S, n = 37, 700
+    table = [splitmix_bytes(97000 + s, 32) for s in range(S)]
+    sess = rng.integers(0, S, n).astype(np.uint32)
+    lens = [int(x) for x in rng.integers(0, 3000, n)]
+    lens[:6] = [0, 1, 63, 128, 1500, 16384]
+    msgs = [splitmix_bytes(98000 + i, L) for i, L in enumerate(lens)]
+    nonces = [splitmix_bytes(99000 + i, 12) for i in range(n)]
+    keys_per = [table[s] for s in sess]
+    ref = seal_frames(enet, msgs, keys_per, nonces, 16, 3)
+    tbl = torch.tensor(np.frombuffer(b"".join(table), np.uint8).copy()).cuda()
+    mid = torch.zeros(16 * S, dtype=torch.int32, device="cuda")
+    enet.hmac_midstates(tbl, S, mid)
+    sess_seal = sess.copy()
+    sess_seal[11] = S + 5  # past the table: sealed with a zero MAC
+    st = torch.tensor(sess_seal.view(np.int32)).cuda()
+    b = dataclasses.replace(enet.make_batch(msgs, keys_per, nonces, base_offset=3), keys=tbl)
+    ooffs = offsets_for([L + 48 for L in lens], 4)
+    out = torch.zeros(int(ooffs[-1]), dtype=torch.uint8, device="cuda")
+    enet.wire_seal_sessions(b, out, torch.tensor(ooffs).cuda(), st, S, mid)
+    got = records_of(host(out), ooffs.tolist())
+    assert got[:11] == ref[:11] and got[12:] == ref[12:]
+    assert got[11] != ref[11] and len(got[11]) == len(ref[11])
+    for i in list(range(0, n, 23)) + [0, 1, 5]:
+        assert got[i] == wire_of(nonces[i], oracle.frame_seal(keys_per[i], nonces[i], msgs[i])), i
+    frames = list(got)
+    frames[5] = frames[5][:20] + bytes([frames[5][20] ^ 0x10]) + frames[5][21:]
+    sess2 = sess.copy()
+    sess2[7] = (sess2[7] + 1) % S
+    sess2[9] = 0xFFFFFFF0  # past the table on open
+    bo = dataclasses.replace(enet.make_batch(frames, keys_per, nonces, base_offset=2), keys=tbl, nonces=None)
+    poffs = offsets_for(lens, 1)
+    pt = torch.full((int(poffs[-1]) + 1,), 0xAA, dtype=torch.uint8, device="cuda")
+    macs = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.wire_open_sessions(bo, pt, torch.tensor(poffs).cuda(), torch.tensor(sess2.view(np.int32)).cuda(),
+                            S, mid, macs, ok)
+    okh = ok.cpu().tolist()
+    back = records_of(host(pt), poffs.tolist())
+    assert [i for i in range(n) if okh[i] == 0] == [5, 7, 9, 11]
+    for i in range(n):
+        assert back[i] == (bytes(lens[i]) if i in (5, 7, 9, 11) else msgs[i]), i
