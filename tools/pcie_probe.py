@@ -51,4 +51,25 @@ for S in (2, 3, 4, 8):
                 h_dst[c * C:(c + 1) * C].copy_(d_a[c * C:(c + 1) * C], non_blocking=True)
 
     out[f"chunk16M_roundtrip_{S}streams_GBs_each_dir"] = N / timed(chunked) / 1e9
+
+# one stream per direction: every H2D chunk back to back on the up stream, the D2H of chunk c on
+# the down stream after an event on the up stream (the copy engines never wait on each other's
+# queue order), for 16 and 64 MiB chunks; K up / K down streams round-robin for K = 2
+for C in (16 << 20, 64 << 20):
+    for K in (1, 2):
+        ups = [torch.cuda.Stream(dev) for _ in range(K)]
+        downs = [torch.cuda.Stream(dev) for _ in range(K)]
+
+        def split():
+            for c in range(N // C):
+                up, down = ups[c % K], downs[c % K]
+                with torch.cuda.stream(up):
+                    d_a[c * C:(c + 1) * C].copy_(h_src[c * C:(c + 1) * C], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(up)
+                down.wait_event(ev)
+                with torch.cuda.stream(down):
+                    h_dst[c * C:(c + 1) * C].copy_(d_a[c * C:(c + 1) * C], non_blocking=True)
+
+        out[f"split_{C >> 20}M_{K}x2streams_GBs_each_dir"] = N / timed(split) / 1e9
 print(json.dumps({k: round(v, 1) for k, v in out.items()}))
