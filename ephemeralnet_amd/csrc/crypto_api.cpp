@@ -969,6 +969,65 @@ std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std:
     return download(st, d, out_off);
 }
 
+namespace {
+// the session table's indices and HMAC midstates on the device (S_AUX, S_CTR: unused by frames)
+std::pair<const uint32_t*, const uint32_t*> upload_sessions(Staging& st, const DevRecords& d,
+                                                            std::span<const std::uint32_t> session, size_t K,
+                                                            const char* what) {
+    for (std::uint32_t s : session)
+        if (s >= K) throw std::invalid_argument(std::string("enet batch::") + what + ": session index outside the table");
+    auto* ds = (uint32_t*)st.get(S_AUX, 4 * session.size());
+    auto* mid = (uint32_t*)st.get(S_CTR, 64 * K);
+    st.h2d(ds, session.data(), 4 * session.size());
+    enet_check(enet_hmac_midstates(d.r.keys, (uint32_t)K, mid, st.s()), what);
+    return {ds, mid};
+}
+}  // namespace
+
+std::vector<std::vector<std::uint8_t>> wire_seal_sessions(std::span<const std::array<std::uint8_t, 32>> session_table,
+                                                          std::span<const std::uint32_t> session,
+                                                          std::span<const Nonce> nonces,
+                                                          std::span<const std::span<const std::uint8_t>> messages) {
+    const size_t n = messages.size(), K = session_table.size();
+    if (session.size() != n || nonces.size() != n || K > 0xffffffffu)
+        throw std::invalid_argument("enet batch::wire_seal_sessions: size mismatch");
+    if (n == 0) return {};
+    if (K == 0) throw std::invalid_argument("enet batch::wire_seal_sessions: session index outside the table");
+    Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
+    Packed in = pack(messages);
+    auto out_off = offsets_of(messages, 16 + 32);
+    auto nf = flat_nonces(nonces);
+    DevRecords d = upload(st, in, out_off, session_table.data()->data(), 32 * K, 32, nf.data(), n);
+    auto [ds, mid] = upload_sessions(st, d, session, K, "wire_seal_sessions");
+    enet_check(enet_wire_seal_batch_sessions(&d.r, ds, (uint32_t)K, mid, st.s()), "wire_seal_sessions");
+    return download(st, d, out_off);
+}
+
+std::vector<std::vector<std::uint8_t>> wire_open_sessions(std::span<const std::array<std::uint8_t, 32>> session_table,
+                                                          std::span<const std::uint32_t> session,
+                                                          std::span<const std::span<const std::uint8_t>> frames,
+                                                          std::vector<std::uint8_t>& ok) {
+    const size_t n = frames.size(), K = session_table.size();
+    if (session.size() != n || K > 0xffffffffu)
+        throw std::invalid_argument("enet batch::wire_open_sessions: size mismatch");
+    ok.assign(n, 0);
+    if (n == 0) return {};
+    if (K == 0) throw std::invalid_argument("enet batch::wire_open_sessions: session index outside the table");
+    Staging& st = staging();
+    st.reset();  // a previous call that threw may have left queued downloads
+    Packed in = pack(frames);
+    auto out_off = offsets_of(frames, -(16 + 32));
+    std::vector<uint8_t> no_nonces(12 * n, 0);  // unused: the nonce travels in the frame
+    DevRecords d = upload(st, in, out_off, session_table.data()->data(), 32 * K, 32, no_nonces.data(), n);
+    auto [ds, mid] = upload_sessions(st, d, session, K, "wire_open_sessions");
+    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
+    auto* dok = (uint8_t*)st.get(S_OK, n);
+    enet_check(enet_wire_open_batch_sessions(&d.r, ds, (uint32_t)K, mid, macs, dok, st.s()), "wire_open_sessions");
+    st.d2h(ok.data(), dok, n);
+    return download(st, d, out_off);
+}
+
 // ------------------------------------------------------------------------------ proof of work
 namespace {
 void put_be64(std::vector<std::uint8_t>& v, std::uint64_t x) {

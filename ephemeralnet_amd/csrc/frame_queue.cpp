@@ -73,12 +73,20 @@ public:
             } catch (const std::system_error&) {  // no thread to be had: serve this frame here
                 lk.unlock();
                 std::vector<Req*> one{&r};
-                const bool host = exec_(one);
+                bool host = false, failed = false;
+                try {
+                    host = exec_(one);
+                } catch (...) {  // as in run(): the frame fails, nothing escapes to the session
+                    failed = true;
+                    r.ok = false;
+                }
                 lk.lock();
                 r.done = true;
-                stats_.frames += 1;
-                stats_.flushes += 1;
-                stats_.host_flushes += host ? 1 : 0;
+                if (!failed) {
+                    stats_.frames += 1;
+                    stats_.flushes += 1;
+                    stats_.host_flushes += host ? 1 : 0;
+                }
                 return;
             }
         }

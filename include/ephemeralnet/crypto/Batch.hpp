@@ -77,6 +77,17 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_seal(
 ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open(
     std::span<const std::array<std::uint8_t, 32>> session_keys,
     std::span<const std::span<const std::uint8_t>> frames, std::vector<std::uint8_t>& ok);
+// The same frames from a table of session keys: frame i belongs to session_table[session[i]]
+// (bytes identical to wire_seal / wire_open with session_keys[i] = session_table[session[i]]).
+// The HMAC key-block midstates are computed once per table entry on the device
+// (enet_hmac_midstates, enet_wire_*_batch_sessions).  Throws std::invalid_argument for a size
+// mismatch or a session index outside the table.
+ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_seal_sessions(
+    std::span<const std::array<std::uint8_t, 32>> session_table, std::span<const std::uint32_t> session,
+    std::span<const Nonce> nonces, std::span<const std::span<const std::uint8_t>> messages);
+ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open_sessions(
+    std::span<const std::array<std::uint8_t, 32>> session_table, std::span<const std::uint32_t> session,
+    std::span<const std::span<const std::uint8_t>> frames, std::vector<std::uint8_t>& ok);
 
 // Cross-session frame queues.  SessionManager runs one detached reader
 // thread per session (SessionManager.cpp:332-333, receive_loop :703-854) and sends from whatever

@@ -117,6 +117,37 @@ int main() {
                               ok[0] == 1 && ok[1] == 1 && back[0] == mb && back[1] == mb &&
                               frames[0] != frames[1];
             std::cout << hex(frames[0]) << " " << (good ? "1" : "0") << "\n";
+        } else if (op == "wire_sessions") {
+            // session-keyed wire frames: a 2-key table, frames filed as sessions {1, 0, 1}; the
+            // bytes equal wire_seal's with per-frame keys, and open rejects a misfiled frame
+            std::string k0, k1, m; in >> k0 >> k1 >> m;
+            std::array<uint8_t, 32> tbl[2]{};
+            auto b0 = unhex(k0), b1 = unhex(k1);
+            std::copy(b0.begin(), b0.end(), tbl[0].begin());
+            std::copy(b1.begin(), b1.end(), tbl[1].begin());
+            auto mb = unhex(m);
+            std::vector<uint8_t> m2(mb.rbegin(), mb.rend());
+            std::span<const uint8_t> ms[3] = {mb, m2, mb};
+            const uint32_t sess[3] = {1, 0, 1};
+            crypto::Nonce nonces[3]{};
+            for (int i = 0; i < 3; ++i) nonces[i].bytes[0] = (uint8_t)(11 + i);
+            auto frames = crypto::batch::wire_seal_sessions(tbl, sess, nonces, ms);
+            std::array<uint8_t, 32> per[3] = {tbl[1], tbl[0], tbl[1]};
+            auto ref = crypto::batch::wire_seal(per, nonces, ms);
+            std::span<const uint8_t> fs[3] = {frames[0], frames[1], frames[2]};
+            const uint32_t sess_open[3] = {1, 0, 0};  // frame 2 misfiled
+            std::vector<uint8_t> ok;
+            auto back = crypto::batch::wire_open_sessions(tbl, sess_open, fs, ok);
+            bool threw = false;
+            const uint32_t bad[3] = {1, 2, 0};
+            try {
+                (void)crypto::batch::wire_seal_sessions(tbl, bad, nonces, ms);
+            } catch (const std::invalid_argument&) {
+                threw = true;
+            }
+            const bool good = frames == ref && ok.size() == 3 && ok[0] == 1 && ok[1] == 1 && ok[2] == 0 &&
+                              back[0] == mb && back[1] == m2 && threw;
+            std::cout << hex(frames[0]) << " " << (good ? "1" : "0") << "\n";
         } else if (op == "chunk_pipe") {
             // Node::store_chunk / fetch_chunk crypto steps over the batch pipeline
             std::string p; in >> p;

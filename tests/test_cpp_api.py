@@ -146,6 +146,12 @@ def test_cpp_api_matches_reference_golden(api_bin, golden):
         m = bytes.fromhex(f["signed"])[:-32]
         ops.append(f"wire_queue {f['key']} {h(m)}")
         expect.append(("wire", (bytes.fromhex(f["key"]), m)))
+    # session-keyed frames: frame 0 is filed under table[1]
+    for f in golden["frames"][:3]:
+        m = bytes.fromhex(f["signed"])[:-32]
+        k0 = hashlib.sha256(bytes.fromhex(f["key"])).hexdigest()
+        ops.append(f"wire_sessions {k0} {f['key']} {h(m)}")
+        expect.append(("wire", (bytes.fromhex(f["key"]), m)))
     for L in (0, 1, 64, 1500, 4096):
         pt = splitmix_bytes(777 + L, L)
         ops.append(f"chunk_pipe {h(pt)}")
