@@ -240,14 +240,14 @@ __global__ __launch_bounds__(kWG) void hmac_midstate_kernel(uint32_t n, const ui
 
 hipError_t launch_hmac_midstates(uint32_t n, const uint8_t* keys, uint32_t* mid, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(hmac_midstate_kernel, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s, n, keys, mid);
+    hipLaunchKernelGGL(hmac_midstate_kernel, dim3((uint32_t)(((uint64_t)n + kWG - 1) / kWG)), dim3(kWG), 0, s, n, keys, mid);
     return hipGetLastError();
 }
 
 hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
                                const int64_t* ticks, uint8_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(session_key_kernel, dim3((n + kWG - 1) / kWG), dim3(kWG), 0, s, n, secrets,
+    hipLaunchKernelGGL(session_key_kernel, dim3((uint32_t)(((uint64_t)n + kWG - 1) / kWG)), dim3(kWG), 0, s, n, secrets,
                        counters, ticks, out);
     return hipGetLastError();
 }
