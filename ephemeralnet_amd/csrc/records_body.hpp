@@ -583,7 +583,17 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             const uint32_t rl = min(kRun, Lu - kRun * st);  // uniform
             uint32_t x[32];
             uint32_t ro = dme + 128u * (st & 1u);
-            if (rl == kRun) {
+            // even stages: the run starts in slot 0 (ro = d < 128) and never wraps, so its dwords
+            // are one base plus immediate offsets; odd stages wrap into slot 0 (ring_at's & 255,
+            // two VALU per dword)
+            if (rl == kRun && (st & 1u) == 0u) {
+                // opaque to the compiler, which otherwise proves the two paths equal and keeps
+                // only the masked one
+                uint32_t eo = ro;
+                asm volatile("" : "+v"(eo));
+#pragma unroll
+                for (int m = 0; m < 32; ++m) x[m] = *reinterpret_cast<const uint32_t*>(myring + eo + 4u * m);
+            } else if (rl == kRun) {
 #pragma unroll
                 for (int m = 0; m < 32; ++m) x[m] = *ring_at(ro, m);
             } else {
@@ -632,7 +642,12 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             }
             // recompute the ring addresses here instead of holding 32 of them across the rounds
             asm volatile("" : "+v"(ro));
-            if (rl == kRun) {
+            if (rl == kRun && (st & 1u) == 0u) {
+                uint32_t eo = ro;
+                asm volatile("" : "+v"(eo));
+#pragma unroll
+                for (int m = 0; m < 32; ++m) *reinterpret_cast<uint32_t*>(myring + eo + 4u * m) = x[m];
+            } else if (rl == kRun) {
 #pragma unroll
                 for (int m = 0; m < 32; ++m) *ring_at(ro, m) = x[m];
             } else {
