@@ -110,19 +110,41 @@ def parse():
     return a
 
 
-def host_threads() -> int:
-    """Threads for the CPU baselines: every core in this process's affinity mask (BASELINE.md 3 /
-    SURVEY 8d: all host cores, the count stated in the line)."""
+def affinity_cpus() -> int:
+    """CPUs in this process's affinity mask (on the GPU box: the whole machine, 256)."""
     try:
         return max(1, len(os.sched_getaffinity(0)))
     except AttributeError:
         return max(1, os.cpu_count() or 1)
 
 
+def cgroup_cpus() -> int | None:
+    """CPUs the cgroup quota grants (cpu.max "quota period" -> ceil(quota / period)), None when
+    unlimited or unreadable.  The GPU box: "1600000 100000" = 16 CPUs of a 256-CPU machine."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+    except (OSError, ValueError):
+        return None
+    if quota == "max":
+        return None
+    q, p = int(quota), int(period)
+    return max(1, -(-q // p)) if q > 0 and p > 0 else None
+
+
+def host_threads() -> int:
+    """Threads for the CPU baselines = the CPUs this process can actually use: the affinity mask
+    capped by the cgroup CPU quota (all host cores, the count stated in the line).
+    Round 3 ran 256 threads under a 16-CPU quota and reported 256 cores."""
+    q = cgroup_cpus()
+    return min(affinity_cpus(), q) if q else affinity_cpus()
+
+
 def host_cpu_info() -> dict:
     """nproc, the affinity mask size, the lscpu model name and the cgroup CPU quota (cpu.max),
     recorded beside every CPU number so the baseline's hardware is explicit."""
-    info = {"nproc": os.cpu_count(), "affinity": host_threads(), "model": None, "cgroup_cpu_max": None}
+    info = {"nproc": os.cpu_count(), "affinity": affinity_cpus(), "cgroup_cpus": cgroup_cpus(),
+            "effective_cpus": host_threads(), "model": None, "cgroup_cpu_max": None}
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -348,6 +370,22 @@ def sample_power(proc, step, sync, secs: float = 2.5) -> dict | None:
             "samples": len(pw[g]),
             "source": "rocm-smi while seal/open pairs run back to back after the timed region "
                       "(busiest GPU); idle sclk 2.4 GHz, package cap ~1.4 kW"}
+
+
+def rank_report(world: int, red_dev, local_bytes: int, local_s: float, local_ok: bool):
+    """N > 1: every rank's own rate and round-trip verdict, all-gathered, plus what the process
+    group itself says (backend, world size), so a SCALE record shows that N ranks each did the
+    same work.  None for a single process."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+    mine = torch.tensor([float(local_bytes), local_s, 1.0 if local_ok else 0.0],
+                        dtype=torch.float64, device=red_dev)
+    got = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, mine)
+    return [{"rank": i, "gibs": round(g[0].item() / g[1].item() / 2**30, 2),
+             "bytes": int(g[0].item()), "ok": bool(g[2].item())} for i, g in enumerate(got)]
 
 
 def dist_init(local: int):
@@ -786,6 +824,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -812,14 +851,21 @@ def main():
     reps = max(4, args.steps)
     seal_ms, open_ms = kernel_ms_alt(reps)
     okh = int(ok.sum().item()) if args.mode != "xor" else n
-    if okh != n:
-        raise SystemExit(f"rank {rank}: {n - okh} records failed to open")
     # the round trip must give the plaintext back, byte for byte (a keystream bug shared by seal
     # and open would still verify every tag), and the ciphertext must differ from it
-    if not torch.equal(back, pt):
-        raise SystemExit(f"rank {rank}: open(seal(x)) != x")
-    if args.mode in ("aead", "xor", "store") and torch.equal(ct, pt):
-        raise SystemExit(f"rank {rank}: ciphertext equals plaintext")
+    fail = None
+    if okh != n:
+        fail = f"rank {rank}: {n - okh} records failed to open"
+    elif not torch.equal(back, pt):
+        fail = f"rank {rank}: open(seal(x)) != x"
+    elif args.mode in ("aead", "xor", "store") and torch.equal(ct, pt):
+        fail = f"rank {rank}: ciphertext equals plaintext"
+    ranks = rank_report(world, red_dev, n * L * args.steps, elapsed_local, fail is None)
+    if fail is not None:
+        raise SystemExit(fail)
+    if ranks is not None and not all(r["ok"] for r in ranks):
+        raise SystemExit(f"rank {rank}: round trip failed on rank(s) "
+                         f"{[r['rank'] for r in ranks if not r['ok']]}")
     power = None
     if sampler is not None:
         power = sample_power(sampler, lambda: (seal(), open_()), lambda: torch.cuda.synchronize(dev))
@@ -934,6 +980,9 @@ def main():
         }
         if power:
             out["power"] = power
+        if ranks is not None:
+            out["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                           "per_rank": ranks}
         if not args.no_cpu_baseline and world == 1:
             if args.mode == "wire":  # the same workload through the reference itself
                 ref = cpu_reference_frames(L, args.cpu_seconds)

@@ -74,6 +74,23 @@ POW_STORE = 1  # candidates = successive mt19937_64 outputs (StoreProof.cpp)
 _lib: Optional[C.CDLL] = None
 
 
+def check_stamp() -> dict:
+    """The in-tree library must have been built from the sources beside it: its stamp
+    (libenet_crypto.so.stamp.json, written by build.py) carries the SHA-256 of the compiler
+    flags, csrc/ and include/.  A stale or unstamped library raises instead of silently running
+    old kernels (ENET_ALLOW_STALE_LIB=1 overrides, e.g. for tools' own builds)."""
+    from . import build as B
+    if os.path.abspath(LIB_PATH) != os.path.abspath(B.LIB) or os.environ.get("ENET_ALLOW_STALE_LIB") == "1":
+        return {}
+    st = B.read_stamp(B.LIB)
+    want = B.source_digest()
+    if st is None or st.get("sources_sha256") != want:
+        raise EnetError(f"{LIB_PATH} was not built from these sources (stamp "
+                        f"{None if st is None else st.get('sources_sha256', '?')[:12]}, sources "
+                        f"{want[:12]}): rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
+    return st
+
+
 def lib() -> C.CDLL:
     """Load the in-tree HIP library (fails loudly when it is missing)."""
     global _lib
@@ -81,6 +98,7 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise EnetError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
                             "g.build()'` (hipcc --offload-arch=gfx950)")
+        check_stamp()
         L = C.CDLL(LIB_PATH)
         vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
         rp = C.POINTER(_Records)
@@ -281,7 +299,7 @@ def hmac_midstates(keys, n: int, mid, stream=None) -> None:
 def wire_seal_sessions(b: Batch, out, out_offsets, session, sessions: int, mid, stream=None) -> None:
     """wire_seal with b.keys a table of `sessions` keys, session[i] (int32) the session of frame i
     and mid the table's hmac_midstates (same bytes as wire_seal with per-frame keys
-    table[session[i]]; an index >= sessions seals that frame with a zero MAC)."""
+    table[session[i]]; an index >= sessions zeroes that frame's whole output slot)."""
     r = b.records(out, out_offsets)
     _check(lib().enet_wire_seal_batch_sessions(C.byref(r), _ptr(session), sessions, _ptr(mid),
                                                _stream(stream)), "enet_wire_seal_batch_sessions")

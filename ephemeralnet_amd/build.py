@@ -3,9 +3,13 @@ the repo snapshot to the GPU box).  Each translation unit compiles to its own ob
 parallel (the device code of one TU never calls into another), then one link step."""
 from __future__ import annotations
 
+import hashlib
+import json
 import os
+import platform
 import subprocess
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
@@ -58,14 +62,46 @@ def _stale_obj(src: str, hdr_t: float, obj_dir: str = OBJ) -> bool:
     return os.path.getmtime(os.path.join(CSRC, src)) > t or hdr_t > t
 
 
+def source_digest(tools: bool = False) -> str:
+    """SHA-256 over the compiler, the flags and the bytes of every source and header the library
+    is built from (csrc/ and include/): what the built .so claims to be in its stamp file."""
+    h = hashlib.sha256()
+    h.update(" ".join([HIPCC] + CFLAGS + LDFLAGS + (["-DENET_TOOLS_BUILD"] if tools else [])).encode())
+    files = [os.path.join(CSRC, f) for f in SOURCES] + _headers()
+    for f in sorted(set(files)):
+        h.update(os.path.relpath(f, ROOT).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def stamp_path(lib: str = LIB) -> str:
+    return lib + ".stamp.json"
+
+
+def read_stamp(lib: str = LIB) -> dict | None:
+    try:
+        with open(stamp_path(lib)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
           tools: bool = False) -> str:
     obj_dir, lib = (OBJ_TOOLS, LIB_TOOLS) if tools else (OBJ, LIB)
     cflags = CFLAGS + (["-DENET_TOOLS_BUILD"] if tools else [])
     os.makedirs(obj_dir, exist_ok=True)
+    digest = source_digest(tools)
+    stamp = read_stamp(lib)
+    # a library whose stamp names other sources is stale whatever the mtimes say (a pushed .so
+    # beside edited sources, a checkout that reset mtimes): rebuild every TU
+    force = force or stamp is None or stamp.get("sources_sha256") != digest
     todo = [s for s in SOURCES if force or _stale_obj(s, _hdr_time(s), obj_dir)]
     if not todo and os.path.exists(lib) and \
             os.path.getmtime(lib) >= max(os.path.getmtime(_obj(s, obj_dir)) for s in SOURCES):
+        print(f"[build] {os.path.relpath(lib, ROOT)} up to date (sources {digest[:12]}, nothing "
+              "recompiled)", file=sys.stderr)
         return lib
 
     def cc(src: str) -> None:
@@ -86,6 +122,15 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, lib)
+    with open(lib, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
+    rec = {"sources_sha256": digest, "lib_sha256": lib_sha, "recompiled": todo,
+           "built_at": time.strftime("%Y-%m-%dT%H:%M:%S%z"), "host": platform.node()}
+    with open(stamp_path(lib) + ".tmp", "w") as f:
+        json.dump(rec, f, indent=1)
+    os.replace(stamp_path(lib) + ".tmp", stamp_path(lib))
+    print(f"[build] {os.path.relpath(lib, ROOT)} rebuilt: recompiled {len(todo)} of {len(SOURCES)} "
+          f"TUs ({', '.join(todo)}), sources {digest[:12]}, lib {lib_sha[:12]}", file=sys.stderr)
     return lib
 
 

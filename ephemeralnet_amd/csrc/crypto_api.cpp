@@ -404,17 +404,31 @@ public:
             std::vector<ChachaReq*> batch;
             batch.swap(pending_);
             lk.unlock();
+            // Whatever leaves the leader section (bad_alloc included), every request it took is
+            // marked done -- ok stays false for the ones not run, so their callers finish on the
+            // host engine -- and the next leader can start (a throw here used to
+            // leave busy_ set and every later device-routed caller waiting forever).
+            struct Release {
+                Coalescer& c;
+                std::unique_lock<std::mutex>& lk;
+                std::vector<ChachaReq*>& batch;
+                ~Release() {
+                    if (!lk.owns_lock()) lk.lock();
+                    for (ChachaReq* q : batch) q->done = true;
+                    c.busy_ = false;
+                    c.cv_.notify_all();
+                }
+            } release{*this, lk, batch};
             // groups that fit the arena; a record larger than the arena alone stays !ok (host)
             size_t i = 0;
             while (i < batch.size()) {
                 size_t j = i, bytes = 0;
                 while (j < batch.size() && (j == i || bytes + batch[j]->n <= kArenaMax)) bytes += batch[j++]->n;
-                std::vector<ChachaReq*> group(batch.begin() + (ptrdiff_t)i, batch.begin() + (ptrdiff_t)j);
                 bool ok = false;
                 if (bytes <= kArenaMax) {
                     try {
                         scalar::maybe_inject();
-                        run(group);
+                        run(batch, i, j);
                         ok = true;
                     } catch (const std::exception& e) {
                         scalar::device_failed("ChaCha20::apply", e.what());
@@ -422,13 +436,9 @@ public:
                         scalar::device_failed("ChaCha20::apply", "unknown error");
                     }
                 }
-                for (ChachaReq* q : group) q->ok = ok;
+                for (size_t q = i; q < j; ++q) batch[q]->ok = ok;
                 i = j;
             }
-            lk.lock();
-            for (ChachaReq* q : batch) q->done = true;
-            busy_ = false;
-            cv_.notify_all();
         }
         return r.ok;
     }
@@ -439,7 +449,8 @@ private:
     // 16 lanes, so a lone 1 MiB record ran on 16 lanes at ~0.5 GB/s.
     static constexpr size_t kSeg = 16u << 10;
 
-    void run(const std::vector<ChachaReq*>& batch) {
+    void run(const std::vector<ChachaReq*>& all, size_t first, size_t last) {
+        const std::span<ChachaReq* const> batch(all.data() + first, last - first);
         size_t nseg = 0;
         uint64_t rec = 0;
         for (const ChachaReq* q : batch) {

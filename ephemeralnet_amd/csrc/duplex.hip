@@ -107,6 +107,13 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         Lm = Li;
         valid = valid && Lo == Li;
     }
+    // session-keyed frames: an index outside the table fails closed -- the record is processed
+    // as invalid (seal: the whole output slot zeroed, no byte encrypted under another session's
+    // key; open: ok = 0, plaintext zeroed), and no key or midstate past the table is read
+    const uint32_t sraw = (p.session && live) ? p.session[rec] : 0u;
+    const bool sbad = p.session && sraw >= p.n_sessions;
+    const uint32_t sid = sbad ? 0u : sraw;
+    valid = valid && !sbad;
     if (!valid) Lm = 0;
     const uint32_t Ts = (uint32_t)(Lm / kRun);         // whole stages
     const uint32_t r = (uint32_t)(Lm - (uint64_t)kRun * Ts);  // ragged end, < 128
@@ -153,11 +160,6 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         return *reinterpret_cast<const uint4*>(d);
     };
 
-    // session-keyed frames: an index outside the table reads session 0 and the frame fails (a
-    // zero MAC on seal, ok = 0 on open) instead of reading past the table
-    const uint32_t sraw = (p.session && live) ? p.session[rec] : 0u;
-    const bool sbad = p.session && sraw >= p.n_sessions;
-    const uint32_t sid = sbad ? 0u : sraw;
     uint32_t kw[8];
     {
         const uint8_t* kp = p.session ? p.keys + 32ull * sid : p.keys + (size_t)p.key_stride * rec;
@@ -420,7 +422,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 sha256_compress(st, x);
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) d[i] = sbad ? 0u : bswap32(st[i]);
+            for (int i = 0; i < 8; ++i) d[i] = bswap32(st[i]);
         }
         if (!OPEN) {
             if (valid) {
@@ -436,7 +438,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
             }
             ENET_DX_BARRIER();  // T2
         } else if (live) {
-            uint32_t diff = (valid && !sbad) ? 0u : 1u;
+            uint32_t diff = valid ? 0u : 1u;
             if (valid) {
                 if (KIND == DK_FRAME) {  // HmacSha256::verify (HmacSha256.cpp:41-54)
                     uint32_t e[8];

@@ -19,6 +19,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <pthread.h>
 #include <random>
 #include <system_error>
 #include <vector>
@@ -214,10 +215,24 @@ bool host_wire_open(const std::uint8_t key[32], std::span<const std::uint8_t> f,
 // machine however many threads ask, which capped every sender.  Each thread here keeps a
 // ChaCha20 keystream generator keyed with 256 bits from std::random_device and re-keyed every
 // 2^20 nonces (the arc4random construction): 12 unpredictable bytes per frame, never reused under
-// one session key.
+// one session key.  fork() copies a thread's generator into the child, so parent and child would
+// hand out the same nonces; a pthread_atfork child handler bumps a generation
+// counter, and a generator whose generation is stale re-keys from std::random_device before its
+// next nonce.
+std::atomic<std::uint32_t> g_fork_generation{0};
+[[maybe_unused]] const int g_atfork_registered = pthread_atfork(nullptr, nullptr, [] {
+    g_fork_generation.fetch_add(1, std::memory_order_relaxed);
+});
+
 class NonceSource {
 public:
     void draw(Nonce& n) {
+        const std::uint32_t gen = g_fork_generation.load(std::memory_order_relaxed);
+        if (gen != gen_) {  // first use, or a forked child: new key, discard buffered keystream
+            gen_ = gen;
+            left_ = 0;
+            pos_ = sizeof(buf_);
+        }
         if (pos_ + 12 > sizeof(buf_)) refill();
         std::memcpy(n.bytes.data(), buf_ + pos_, 12);
         std::memset(buf_ + pos_, 0, 12);
@@ -250,7 +265,7 @@ private:
     static constexpr std::uint32_t kBlocks = 16;                      // keystream blocks per fill
     static constexpr std::uint32_t kPerFill = kBlocks * 64 / 12;     // 85 nonces per fill
     std::uint8_t key_[32] = {}, iv_[12] = {};
-    std::uint32_t ctr_ = 0, left_ = 0;
+    std::uint32_t ctr_ = 0, left_ = 0, gen_ = 0;
     std::uint8_t buf_[kBlocks * 64] = {};
     std::size_t pos_ = sizeof(buf_);
 };

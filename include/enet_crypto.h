@@ -133,8 +133,9 @@ ENET_API int enet_wire_open_batch(const enet_records* r, uint8_t* macs, uint8_t*
  * enet_hmac_midstates ([sessions][16] uint32).  Same bytes as enet_wire_seal_batch /
  * enet_wire_open_batch with keys[i] = table[session[i]]; every frame skips the two key-block
  * compressions of its HMAC (2 of 27 for a 1 500-byte message).  A session[i] >= sessions
- * (device-resident, so not checked on the host) never reads past the table: seal writes that
- * frame with an all-zero MAC (it never authenticates), open reports ok[i] = 0.  enet_hmac_midstates: for each of
+ * (device-resident, so not checked on the host) never reads past the table and fails closed:
+ * seal zeroes that frame's whole output slot (nothing is encrypted under another session's key),
+ * open reports ok[i] = 0 and zeroes the message.  enet_hmac_midstates: for each of
  * n keys the SHA-256 states after (key || 0^32) ^ ipad and ^ opad (HmacSha256.cpp:11-39). */
 ENET_API int enet_hmac_midstates(const uint8_t* keys, uint32_t n, uint32_t* mid, void* stream);
 ENET_API int enet_wire_seal_batch_sessions(const enet_records* r, const uint32_t* session,

@@ -8,6 +8,9 @@
 #include <string>
 #include <vector>
 
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include "ephemeralnet/crypto/Batch.hpp"
 #include "ephemeralnet/crypto/ChaCha20.hpp"
 #include "ephemeralnet/crypto/CryptoManager.hpp"
@@ -294,6 +297,33 @@ int main() {
             std::vector<uint8_t> buf = unhex(p);
             crypto::ChaCha20::apply(key, nonce, buf, buf, (uint32_t)std::stoul(c));
             std::cout << hex(buf) << "\n";
+        } else if (op == "fork_nonces") {
+            // the frame nonce generator after fork(): parent and child each seal one frame (host
+            // engine, FrameQueue::seal) from a generator that was in use before the fork; the
+            // child's nonce goes back through a pipe.  Prints parent nonce, child nonce, 1/0 distinct
+            std::array<uint8_t, 32> key{};
+            key[0] = 1;
+            std::vector<uint8_t> m(40, 0x5a);
+            crypto::batch::FrameQueue q;
+            (void)q.seal(key, m);  // the generator holds buffered keystream now
+            int fd[2];
+            if (pipe(fd) != 0) { std::cout << "pipe-failed\n"; continue; }
+            const pid_t pid = fork();
+            if (pid == 0) {
+                auto f = q.seal(key, m);
+                const ssize_t w = f ? write(fd[1], f->data(), 12) : -1;
+                _exit(w == 12 ? 0 : 1);
+            }
+            auto f = q.seal(key, m);
+            uint8_t child[12] = {};
+            const ssize_t r = read(fd[0], child, 12);
+            int status = 1;
+            waitpid(pid, &status, 0);
+            close(fd[0]);
+            close(fd[1]);
+            std::vector<uint8_t> pn(f->begin(), f->begin() + 12), cn(child, child + 12);
+            std::cout << hex(pn) << " " << hex(cn) << " "
+                      << (r == 12 && status == 0 && pn != cn ? "1" : "0") << "\n";
         } else if (!op.empty()) {
             std::cout << "?\n";
         }

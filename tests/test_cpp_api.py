@@ -135,6 +135,16 @@ def test_cpp_scalar_api_device_failure_finishes_on_host(api_bin, golden):
     assert err.count("finished on the host engine") == 1
 
 
+def test_cpp_frame_nonces_differ_after_fork(api_bin):
+    """the per-thread frame-nonce generator is copied by fork(); a pthread_atfork
+    handler makes the child re-key, so parent and child never hand out the same nonce (the
+    reference drew every nonce from std::random_device, SessionManager.cpp:365-371)."""
+    for _ in range(3):
+        res, _ = run_ops(api_bin, ["policy host", "fork_nonces"])
+        parent, child, flag = res[1].split()
+        assert flag == "1" and parent != child and len(parent) == len(child) == 24
+
+
 @pytest.mark.gpu
 def test_cpp_api_matches_reference_golden(api_bin, golden):
     ops, expect = scalar_ops(golden, big=True)

@@ -480,8 +480,8 @@ def test_wire_frames_sessions_vs_per_frame_keys(enet):
     computed once (enet_hmac_midstates) instead of the two key-block compressions per frame.
     Bit-exact with the per-frame-key path (keys[i] = table[session[i]]) and with the oracle's
     SessionManager::send restatement; opening accepts every frame, rejects a tampered body, a
-    frame filed under another session and session indices past the table (seal: zero MAC, open:
-    ok = 0 -- never a read past the table), and zeroes their plaintext."""
+    frame filed under another session and session indices past the table (seal: the whole frame
+    slot zeroed, open: ok = 0 -- never a read past the table), and zeroes their plaintext."""
     import torch
     rng = np.random.default_rng(9)
     S, n = 37, 700
@@ -497,7 +497,7 @@ def test_wire_frames_sessions_vs_per_frame_keys(enet):
     mid = torch.zeros(16 * S, dtype=torch.int32, device="cuda")
     enet.hmac_midstates(tbl, S, mid)
     sess_seal = sess.copy()
-    sess_seal[11] = S + 5  # past the table: sealed with a zero MAC
+    sess_seal[11] = S + 5  # past the table: the frame slot comes out all zeros
     st = torch.tensor(sess_seal.view(np.int32)).cuda()
     b = dataclasses.replace(enet.make_batch(msgs, keys_per, nonces, base_offset=3), keys=tbl)
     ooffs = offsets_for([L + 48 for L in lens], 4)
@@ -505,7 +505,8 @@ def test_wire_frames_sessions_vs_per_frame_keys(enet):
     enet.wire_seal_sessions(b, out, torch.tensor(ooffs).cuda(), st, S, mid)
     got = records_of(host(out), ooffs.tolist())
     assert got[:11] == ref[:11] and got[12:] == ref[12:]
-    assert got[11] != ref[11] and len(got[11]) == len(ref[11])
+    # fail closed: nothing of frame 11 is encrypted under another session's key
+    assert got[11] == bytes(len(ref[11]))
     for i in list(range(0, n, 23)) + [0, 1, 5]:
         assert got[i] == wire_of(nonces[i], oracle.frame_seal(keys_per[i], nonces[i], msgs[i])), i
     frames = list(got)

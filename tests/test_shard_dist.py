@@ -74,3 +74,39 @@ def test_two_rank_gloo_union_equals_single_rank():
         pt = splitmix_bytes(1000 + i, lens[i])
         c, t = oracle.aead_seal(splitmix_bytes(2000 + i, 32), splitmix_bytes(3000 + i, 12), pt)
         assert ct == c and tag == t
+
+
+def _report_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r moved (r + 1) GiB in 0.5 s; rank 1 reports a failed round trip
+    ranks = bench.rank_report(world, torch.device("cpu"), (rank + 1) << 30, 0.5, rank != 1)
+    q.put((rank, ranks, dist.get_backend(), dist.get_world_size()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_rank_report_two_rank_gloo():
+    """bench.py's N > 1 reporting: every rank all-gathers each rank's own
+    rate and round-trip verdict, so rank 0's line shows both ranks and a failure on rank 1."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_report_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ranks, backend, ws in res:
+        assert backend == "gloo" and ws == 2
+        assert [r["rank"] for r in ranks] == [0, 1]
+        assert [r["gibs"] for r in ranks] == [2.0, 4.0]
+        assert [r["ok"] for r in ranks] == [True, False]
+    import bench
+    assert bench.rank_report(1, None, 1, 1.0, True) is None
