@@ -61,7 +61,8 @@ EXPORTS = [
     "enet_last_error",
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
-    "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_host_alloc",
+    "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_pipeline_wire_seal",
+    "enet_pipeline_wire_open", "enet_host_set_mode", "enet_host_mode", "enet_host_alloc",
     "enet_host_free", "enet_pipeline_group_create", "enet_pipeline_group_destroy",
     "enet_pipeline_group_size", "enet_pipeline_group_chacha20_xor", "enet_pipeline_group_aead_seal",
     "enet_pipeline_group_aead_open", "enet_pipeline_group_aead_hmac_seal",
@@ -135,6 +136,9 @@ def lib() -> C.CDLL:
         L.enet_pipeline_aead_open.argtypes = [vp, rp, vp, vp]
         L.enet_pipeline_aead_hmac_seal.argtypes = [vp, rp, vp, vp]
         L.enet_pipeline_aead_hmac_open.argtypes = [vp, rp, vp, vp, vp]
+        L.enet_pipeline_wire_seal.argtypes = [vp, rp]
+        L.enet_pipeline_wire_open.argtypes = [vp, rp, vp]
+        L.enet_host_set_mode.argtypes = [C.c_int]
         L.enet_pipeline_group_create.argtypes = [vp, u32, u64, u32]
         L.enet_pipeline_group_create.restype = vp
         L.enet_pipeline_group_destroy.argtypes = [vp]
@@ -373,6 +377,15 @@ def set_staging(variant: int) -> None:
     _check(lib().enet_set_staging(variant), "enet_set_staging")
 
 
+def set_host_mode(mode: int) -> None:
+    """Host-resident batches: 0 = zero-copy kernels on pinned host memory, 1 = SDMA copies."""
+    _check(lib().enet_host_set_mode(mode), "enet_host_set_mode")
+
+
+def host_mode() -> int:
+    return int(lib().enet_host_mode())
+
+
 def set_duplex_split(mode: int) -> None:
     """Chunk / AEAD+HMAC duplex paths: 1 = split each record over cipher, schedule and rounds
     waves, 0 = one cipher + one hash lane, -1 = automatic (longest record >= 16 KiB in a uniform
@@ -459,6 +472,20 @@ class Pipeline:
 
     def aead_hmac_open(self, b: Batch, out, tags, macs, ok) -> None:
         self._run("aead_hmac_open", b, out, tags, macs, ok)
+
+    def _run_out(self, op: str, b: Batch, out, out_offsets, *ptrs) -> None:
+        r = b.records(out, out_offsets)
+        fn, name = self._fn(op)
+        _check(fn(self._p, C.byref(r), *[_ptr(p) for p in ptrs]), name)
+
+    def wire_seal(self, b: Batch, frames, frame_offsets) -> None:
+        """Wire frames nonce || BE32 || ChaCha20(m || HMAC(m)) of b's messages (frame_offsets:
+        |m_i| + 48 each), host memory in and out."""
+        self._run_out("wire_seal", b, frames, frame_offsets)
+
+    def wire_open(self, b: Batch, out, out_offsets, ok) -> None:
+        """b.arena holds wire frames; out gets the messages (out_offsets: |f_i| - 48 each)."""
+        self._run_out("wire_open", b, out, out_offsets, ok)
 
 
 class PipelineGroup(Pipeline):

@@ -23,8 +23,9 @@ LIB_TOOLS = os.path.join(PKG, "libenet_crypto_tools.so")
 OBJ_TOOLS = os.path.join(PKG, "build_tools")
 SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "duplex_split.hip", "capi.cpp",
            "crypto_api.cpp",
-           "pipeline.cpp", "host_engine.cpp", "frame_queue.cpp"]
-HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "host_engine.hpp", "scalar.hpp"]
+           "pipeline.cpp", "host_engine.cpp", "frame_queue.cpp", "host_batch.cpp"]
+HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "host_engine.hpp", "scalar.hpp",
+           "host_batch.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC",
           "-fvisibility=hidden", "-Wall", "-Wno-unused-function",

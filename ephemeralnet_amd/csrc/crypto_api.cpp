@@ -41,6 +41,7 @@
 #include <vector>
 
 #include "enet_crypto.h"
+#include "host_batch.hpp"
 #include "host_engine.hpp"
 #include "scalar.hpp"
 
@@ -249,64 +250,9 @@ std::vector<uint64_t> offsets_of(std::span<const std::span<const uint8_t>> items
     return off;
 }
 
-struct DevRecords {
-    enet_records r{};
-    uint8_t* out = nullptr;
-    uint64_t out_total = 0;
-};
-
-// Upload arenas, offsets, keys and nonces; returns the descriptor pointing at device copies.
-DevRecords upload(Staging& st, const Packed& in, const std::vector<uint64_t>& out_off,
-                  const uint8_t* keys, size_t key_bytes, uint32_t key_stride, const uint8_t* nonces,
-                  size_t n) {
-    DevRecords d;
-    auto* din = (uint8_t*)st.get(S_IN, in.arena.size());
-    d.out_total = out_off.back();
-    d.out = (uint8_t*)st.get(S_OUT, d.out_total);
-    auto* dinoff = (uint64_t*)st.get(S_INOFF, in.off.size() * 8);
-    auto* doutoff = (uint64_t*)st.get(S_OUTOFF, out_off.size() * 8);
-    auto* dkeys = (uint8_t*)st.get(S_KEYS, key_bytes);
-    auto* dnon = (uint8_t*)st.get(S_NONCES, 12 * n);
-    st.h2d(din, in.arena.data(), in.arena.size());
-    st.h2d(dinoff, in.off.data(), in.off.size() * 8);
-    st.h2d(doutoff, out_off.data(), out_off.size() * 8);
-    st.h2d(dkeys, keys, key_bytes);
-    st.h2d(dnon, nonces, 12 * n);
-    d.r.count = (uint32_t)n;
-    d.r.in_offsets = dinoff;
-    d.r.out_offsets = doutoff;
-    d.r.in = din;
-    d.r.out = d.out;
-    d.r.keys = dkeys;
-    d.r.key_stride = key_stride;
-    d.r.nonces = dnon;
-    d.r.total_bytes_hint = in.arena.size();
-    uint64_t mx = 0;
-    for (size_t i = 0; i < n; ++i) mx = std::max(mx, in.off[i + 1] - in.off[i]);
-    d.r.max_len_hint = (uint32_t)std::min<uint64_t>(mx, 0xffffffffu);
-    return d;
-}
-
-std::vector<std::vector<uint8_t>> download(Staging& st, const DevRecords& d,
-                                           const std::vector<uint64_t>& out_off) {
-    std::vector<uint8_t> all(d.out_total);
-    st.d2h(all.data(), d.out, d.out_total);
-    st.sync();
-    std::vector<std::vector<uint8_t>> res(out_off.size() - 1);
-    for (size_t i = 0; i + 1 < out_off.size(); ++i)
-        res[i].assign(all.begin() + (ptrdiff_t)out_off[i], all.begin() + (ptrdiff_t)out_off[i + 1]);
-    return res;
-}
-
 std::vector<uint8_t> flat_keys(std::span<const ephemeralnet::crypto::Key> keys) {
     std::vector<uint8_t> v(32 * keys.size());
     for (size_t i = 0; i < keys.size(); ++i) std::memcpy(v.data() + 32 * i, keys[i].bytes.data(), 32);
-    return v;
-}
-
-std::vector<uint8_t> flat_nonces(std::span<const ephemeralnet::crypto::Nonce> nonces) {
-    std::vector<uint8_t> v(12 * nonces.size());
-    for (size_t i = 0; i < nonces.size(); ++i) std::memcpy(v.data() + 12 * i, nonces[i].bytes.data(), 12);
     return v;
 }
 
@@ -759,27 +705,75 @@ std::optional<ChunkData> CryptoManager::decrypt_with_key(const Key& key, const C
 // ------------------------------------------------------------------------------ batch
 namespace batch {
 
+namespace {
+static_assert(sizeof(Key) == 32 && sizeof(Nonce) == 12 && sizeof(ChunkId) == 32,
+              "crypto::Key / Nonce / ChunkId are passed to the device as packed arrays");
+const std::uint8_t* key_bytes(std::span<const Key> k) { return reinterpret_cast<const std::uint8_t*>(k.data()); }
+const std::uint8_t* nonce_bytes(std::span<const Nonce> n) { return reinterpret_cast<const std::uint8_t*>(n.data()); }
+
+// One batch call through the host-memory runtime of the calling thread's device (host_batch.hpp):
+// pinned, device-mapped staging, host worker threads gathering / scattering, chunks overlapped.
+void run_host_batch(const enet::hb::Job& j) {
+    int dev = 0;
+    hip_check(hipGetDevice(&dev), "hipGetDevice");
+    enet::hb::run(enet::hb::shared_engine(dev), j);
+}
+
+enet::hb::Job job_of(enet::hb::Op op, std::span<const std::span<const std::uint8_t>> in) {
+    enet::hb::Job j;
+    j.op = op;
+    j.n = in.size();
+    j.in_spans = in;
+    return j;
+}
+
+// contiguous output of a batch call: record i at offsets[i], the prefix sums of the op's lengths
+std::vector<std::uint64_t> out_offsets_for(std::span<const std::span<const std::uint8_t>> in, std::int64_t delta,
+                                           std::size_t out_size, const char* what) {
+    auto off = offsets_of(in, delta);
+    if (off.back() > out_size)
+        throw std::invalid_argument(std::string("enet batch::") + what + ": output span too small");
+    return off;
+}
+}  // namespace
+
+std::vector<std::uint64_t> packed_offsets(std::span<const std::span<const std::uint8_t>> records,
+                                          std::int64_t delta) {
+    return offsets_of(records, delta);
+}
+
 std::vector<std::vector<std::uint8_t>> chacha20_apply(std::span<const Key> keys, std::span<const Nonce> nonces,
                                                       std::span<const std::span<const std::uint8_t>> inputs,
                                                       std::span<const std::uint32_t> counters) {
     const size_t n = inputs.size();
     if (keys.size() != n || nonces.size() != n || (!counters.empty() && counters.size() != n))
         throw std::invalid_argument("enet batch::chacha20_apply: size mismatch");
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(inputs);
-    auto kf = flat_keys(keys);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
-    const uint32_t* dctr = nullptr;
-    if (!counters.empty()) {
-        auto* c = (uint32_t*)st.get(S_CTR, 4 * n);
-        st.h2d(c, counters.data(), 4 * n);
-        dctr = c;
-    }
-    enet_check(enet_chacha20_xor_batch(&d.r, dctr, st.s()), "chacha20");
-    return download(st, d, in.off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::Xor, inputs);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.counters = counters.empty() ? nullptr : counters.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
+}
+
+void chacha20_apply(std::span<const Key> keys, std::span<const Nonce> nonces,
+                    std::span<const std::span<const std::uint8_t>> inputs, std::span<const std::uint32_t> counters,
+                    std::span<std::uint8_t> out) {
+    const size_t n = inputs.size();
+    if (keys.size() != n || nonces.size() != n || (!counters.empty() && counters.size() != n))
+        throw std::invalid_argument("enet batch::chacha20_apply: size mismatch");
+    if (n == 0) return;
+    const auto off = out_offsets_for(inputs, 0, out.size(), "chacha20_apply");
+    auto j = job_of(enet::hb::Op::Xor, inputs);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.counters = counters.empty() ? nullptr : counters.data();
+    j.out_base = out.data();
+    j.out_off = off.data();
+    run_host_batch(j);
 }
 
 std::vector<Sealed> aead_seal(std::span<const Key> keys, std::span<const Nonce> nonces,
@@ -787,23 +781,37 @@ std::vector<Sealed> aead_seal(std::span<const Key> keys, std::span<const Nonce> 
     const size_t n = plaintexts.size();
     if (keys.size() != n || nonces.size() != n) throw std::invalid_argument("enet batch::aead_seal: size mismatch");
     if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(plaintexts);
-    auto kf = flat_keys(keys);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
-    auto* tags = (uint8_t*)st.get(S_TAGS, 16 * n);
-    enet_check(enet_aead_seal_batch(&d.r, nullptr, nullptr, tags, st.s()), "aead_seal");
-    std::vector<uint8_t> th(16 * n);
-    st.d2h(th.data(), tags, 16 * n);
-    auto data = download(st, d, in.off);
+    std::vector<std::vector<std::uint8_t>> data;
+    std::vector<std::uint8_t> th(16 * n);
+    auto j = job_of(enet::hb::Op::AeadSeal, plaintexts);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.out_vecs = &data;
+    j.tags_out = th.data();
+    run_host_batch(j);
     std::vector<Sealed> res(n);
     for (size_t i = 0; i < n; ++i) {
         res[i].data = std::move(data[i]);
         std::memcpy(res[i].tag.data(), th.data() + 16 * i, 16);
     }
     return res;
+}
+
+void aead_seal(std::span<const Key> keys, std::span<const Nonce> nonces,
+               std::span<const std::span<const std::uint8_t>> plaintexts, std::span<std::uint8_t> out,
+               std::span<std::array<std::uint8_t, 16>> tags) {
+    const size_t n = plaintexts.size();
+    if (keys.size() != n || nonces.size() != n || tags.size() != n)
+        throw std::invalid_argument("enet batch::aead_seal: size mismatch");
+    if (n == 0) return;
+    const auto off = out_offsets_for(plaintexts, 0, out.size(), "aead_seal");
+    auto j = job_of(enet::hb::Op::AeadSeal, plaintexts);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.out_base = out.data();
+    j.out_off = off.data();
+    j.tags_out = tags.data()->data();
+    run_host_batch(j);
 }
 
 std::vector<std::vector<std::uint8_t>> aead_open(std::span<const Key> keys, std::span<const Nonce> nonces,
@@ -814,19 +822,35 @@ std::vector<std::vector<std::uint8_t>> aead_open(std::span<const Key> keys, std:
     if (keys.size() != n || nonces.size() != n || tags.size() != n)
         throw std::invalid_argument("enet batch::aead_open: size mismatch");
     ok.assign(n, 0);
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(ciphertexts);
-    auto kf = flat_keys(keys);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
-    auto* dt = (uint8_t*)st.get(S_TAGS, 16 * n);
-    auto* dok = (uint8_t*)st.get(S_OK, n);
-    st.h2d(dt, tags.data(), 16 * n);
-    enet_check(enet_aead_open_batch(&d.r, nullptr, nullptr, dt, dok, st.s()), "aead_open");
-    st.d2h(ok.data(), dok, n);
-    return download(st, d, in.off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::AeadOpen, ciphertexts);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.tags_in = tags.data()->data();
+    j.ok_out = ok.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
+}
+
+void aead_open(std::span<const Key> keys, std::span<const Nonce> nonces,
+               std::span<const std::span<const std::uint8_t>> ciphertexts,
+               std::span<const std::array<std::uint8_t, 16>> tags, std::span<std::uint8_t> out,
+               std::span<std::uint8_t> ok) {
+    const size_t n = ciphertexts.size();
+    if (keys.size() != n || nonces.size() != n || tags.size() != n || ok.size() != n)
+        throw std::invalid_argument("enet batch::aead_open: size mismatch");
+    if (n == 0) return;
+    const auto off = out_offsets_for(ciphertexts, 0, out.size(), "aead_open");
+    auto j = job_of(enet::hb::Op::AeadOpen, ciphertexts);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.tags_in = tags.data()->data();
+    j.ok_out = ok.data();
+    j.out_base = out.data();
+    j.out_off = off.data();
+    run_host_batch(j);
 }
 
 std::vector<std::array<std::uint8_t, 32>> sha256(std::span<const std::span<const std::uint8_t>> messages) {
@@ -853,15 +877,14 @@ std::vector<std::vector<std::uint8_t>> frame_seal(std::span<const std::array<std
     const size_t n = messages.size();
     if (session_keys.size() != n || nonces.size() != n)
         throw std::invalid_argument("enet batch::frame_seal: size mismatch");
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(messages);
-    auto out_off = offsets_of(messages, 32);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
-    enet_check(enet_frame_seal_batch(&d.r, st.s()), "frame_seal");
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::FrameSeal, messages);
+    j.keys = session_keys.data()->data();
+    j.nonces = nonce_bytes(nonces);
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
 }
 
 std::vector<std::vector<std::uint8_t>> frame_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
@@ -872,18 +895,15 @@ std::vector<std::vector<std::uint8_t>> frame_open(std::span<const std::array<std
     if (session_keys.size() != n || nonces.size() != n)
         throw std::invalid_argument("enet batch::frame_open: size mismatch");
     ok.assign(n, 0);
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(bodies);
-    auto out_off = offsets_of(bodies, -32);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
-    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
-    auto* dok = (uint8_t*)st.get(S_OK, n);
-    enet_check(enet_frame_open_batch(&d.r, macs, dok, st.s()), "frame_open");
-    st.d2h(ok.data(), dok, n);
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::FrameOpen, bodies);
+    j.keys = session_keys.data()->data();
+    j.nonces = nonce_bytes(nonces);
+    j.ok_out = ok.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
 }
 
 std::vector<StoredChunk> chunk_store(std::span<const Key> keys, std::span<const Nonce> nonces,
@@ -893,22 +913,15 @@ std::vector<StoredChunk> chunk_store(std::span<const Key> keys, std::span<const 
     if (keys.size() != n || nonces.size() != n || (!chunk_ids.empty() && chunk_ids.size() != n))
         throw std::invalid_argument("enet batch::chunk_store: size mismatch");
     if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(chunks);
-    auto kf = flat_keys(keys);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
-    auto* hashes = (uint8_t*)st.get(S_TAGS, 32 * n);
-    uint8_t* ids = nullptr;
-    if (!chunk_ids.empty()) {
-        ids = (uint8_t*)st.get(S_AUX, 32 * n);
-        st.h2d(ids, chunk_ids.data(), 32 * n);
-    }
-    enet_check(enet_chunk_store_batch(&d.r, ids, hashes, st.s()), "chunk_store");
-    std::vector<uint8_t> hh(32 * n);
-    st.d2h(hh.data(), hashes, 32 * n);
-    auto data = download(st, d, in.off);
+    std::vector<std::vector<std::uint8_t>> data;
+    std::vector<std::uint8_t> hh(32 * n);
+    auto j = job_of(enet::hb::Op::ChunkStore, chunks);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.ids = chunk_ids.empty() ? nullptr : chunk_ids.data()->data();
+    j.macs_out = hh.data();
+    j.out_vecs = &data;
+    run_host_batch(j);
     std::vector<StoredChunk> res(n);
     for (size_t i = 0; i < n; ++i) {
         res[i].data = std::move(data[i]);
@@ -926,21 +939,17 @@ std::vector<std::vector<std::uint8_t>> chunk_fetch(std::span<const Key> keys, st
     if (keys.size() != n || nonces.size() != n || chunk_ids.size() != n || chunk_hashes.size() != n)
         throw std::invalid_argument("enet batch::chunk_fetch: size mismatch");
     ok.assign(n, 0);
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(ciphertexts);
-    auto kf = flat_keys(keys);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, in.off, kf.data(), kf.size(), 32, nf.data(), n);
-    auto* ids = (uint8_t*)st.get(S_AUX, 32 * n);
-    auto* hashes = (uint8_t*)st.get(S_TAGS, 32 * n);
-    auto* dok = (uint8_t*)st.get(S_OK, n);
-    st.h2d(ids, chunk_ids.data(), 32 * n);
-    st.h2d(hashes, chunk_hashes.data(), 32 * n);
-    enet_check(enet_chunk_fetch_batch(&d.r, ids, hashes, dok, st.s()), "chunk_fetch");
-    st.d2h(ok.data(), dok, n);
-    return download(st, d, in.off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::ChunkFetch, ciphertexts);
+    j.keys = key_bytes(keys);
+    j.nonces = nonce_bytes(nonces);
+    j.ids = chunk_ids.data()->data();
+    j.macs_in = chunk_hashes.data()->data();
+    j.ok_out = ok.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
 }
 
 std::vector<std::vector<std::uint8_t>> wire_seal(std::span<const std::array<std::uint8_t, 32>> session_keys,
@@ -949,15 +958,29 @@ std::vector<std::vector<std::uint8_t>> wire_seal(std::span<const std::array<std:
     const size_t n = messages.size();
     if (session_keys.size() != n || nonces.size() != n)
         throw std::invalid_argument("enet batch::wire_seal: size mismatch");
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(messages);
-    auto out_off = offsets_of(messages, 16 + 32);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, nf.data(), n);
-    enet_check(enet_wire_seal_batch(&d.r, st.s()), "wire_seal");
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::WireSeal, messages);
+    j.keys = session_keys.data()->data();
+    j.nonces = nonce_bytes(nonces);
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
+}
+
+void wire_seal(std::span<const std::array<std::uint8_t, 32>> session_keys, std::span<const Nonce> nonces,
+               std::span<const std::span<const std::uint8_t>> messages, std::span<std::uint8_t> frames) {
+    const size_t n = messages.size();
+    if (session_keys.size() != n || nonces.size() != n)
+        throw std::invalid_argument("enet batch::wire_seal: size mismatch");
+    if (n == 0) return;
+    const auto off = out_offsets_for(messages, 48, frames.size(), "wire_seal");
+    auto j = job_of(enet::hb::Op::WireSeal, messages);
+    j.keys = session_keys.data()->data();
+    j.nonces = nonce_bytes(nonces);
+    j.out_base = frames.data();
+    j.out_off = off.data();
+    run_host_batch(j);
 }
 
 std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
@@ -966,32 +989,35 @@ std::vector<std::vector<std::uint8_t>> wire_open(std::span<const std::array<std:
     const size_t n = frames.size();
     if (session_keys.size() != n) throw std::invalid_argument("enet batch::wire_open: size mismatch");
     ok.assign(n, 0);
-    if (n == 0) return {};
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(frames);
-    auto out_off = offsets_of(frames, -(16 + 32));
-    std::vector<uint8_t> no_nonces(12 * n, 0);  // unused: the nonce travels in the frame
-    DevRecords d = upload(st, in, out_off, session_keys.data()->data(), 32 * n, 32, no_nonces.data(), n);
-    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
-    auto* dok = (uint8_t*)st.get(S_OK, n);
-    enet_check(enet_wire_open_batch(&d.r, macs, dok, st.s()), "wire_open");
-    st.d2h(ok.data(), dok, n);
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    auto j = job_of(enet::hb::Op::WireOpen, frames);
+    j.keys = session_keys.data()->data();
+    j.ok_out = ok.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
+}
+
+void wire_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
+               std::span<const std::span<const std::uint8_t>> frames, std::span<std::uint8_t> messages,
+               std::span<std::uint8_t> ok) {
+    const size_t n = frames.size();
+    if (session_keys.size() != n || ok.size() != n) throw std::invalid_argument("enet batch::wire_open: size mismatch");
+    if (n == 0) return;
+    const auto off = out_offsets_for(frames, -48, messages.size(), "wire_open");
+    auto j = job_of(enet::hb::Op::WireOpen, frames);
+    j.keys = session_keys.data()->data();
+    j.ok_out = ok.data();
+    j.out_base = messages.data();
+    j.out_off = off.data();
+    run_host_batch(j);
 }
 
 namespace {
-// the session table's indices and HMAC midstates on the device (S_AUX, S_CTR: unused by frames)
-std::pair<const uint32_t*, const uint32_t*> upload_sessions(Staging& st, const DevRecords& d,
-                                                            std::span<const std::uint32_t> session, size_t K,
-                                                            const char* what) {
+void check_sessions(std::span<const std::uint32_t> session, size_t K, const char* what) {
     for (std::uint32_t s : session)
         if (s >= K) throw std::invalid_argument(std::string("enet batch::") + what + ": session index outside the table");
-    auto* ds = (uint32_t*)st.get(S_AUX, 4 * session.size());
-    auto* mid = (uint32_t*)st.get(S_CTR, 64 * K);
-    st.h2d(ds, session.data(), 4 * session.size());
-    enet_check(enet_hmac_midstates(d.r.keys, (uint32_t)K, mid, st.s()), what);
-    return {ds, mid};
 }
 }  // namespace
 
@@ -1002,17 +1028,17 @@ std::vector<std::vector<std::uint8_t>> wire_seal_sessions(std::span<const std::a
     const size_t n = messages.size(), K = session_table.size();
     if (session.size() != n || nonces.size() != n || K > 0xffffffffu)
         throw std::invalid_argument("enet batch::wire_seal_sessions: size mismatch");
-    if (n == 0) return {};
-    if (K == 0) throw std::invalid_argument("enet batch::wire_seal_sessions: session index outside the table");
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(messages);
-    auto out_off = offsets_of(messages, 16 + 32);
-    auto nf = flat_nonces(nonces);
-    DevRecords d = upload(st, in, out_off, session_table.data()->data(), 32 * K, 32, nf.data(), n);
-    auto [ds, mid] = upload_sessions(st, d, session, K, "wire_seal_sessions");
-    enet_check(enet_wire_seal_batch_sessions(&d.r, ds, (uint32_t)K, mid, st.s()), "wire_seal_sessions");
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    check_sessions(session, K, "wire_seal_sessions");
+    auto j = job_of(enet::hb::Op::WireSeal, messages);
+    j.keys = session_table.data()->data();
+    j.session = session.data();
+    j.n_sessions = (std::uint32_t)K;
+    j.nonces = nonce_bytes(nonces);
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
 }
 
 std::vector<std::vector<std::uint8_t>> wire_open_sessions(std::span<const std::array<std::uint8_t, 32>> session_table,
@@ -1023,20 +1049,17 @@ std::vector<std::vector<std::uint8_t>> wire_open_sessions(std::span<const std::a
     if (session.size() != n || K > 0xffffffffu)
         throw std::invalid_argument("enet batch::wire_open_sessions: size mismatch");
     ok.assign(n, 0);
-    if (n == 0) return {};
-    if (K == 0) throw std::invalid_argument("enet batch::wire_open_sessions: session index outside the table");
-    Staging& st = staging();
-    st.reset();  // a previous call that threw may have left queued downloads
-    Packed in = pack(frames);
-    auto out_off = offsets_of(frames, -(16 + 32));
-    std::vector<uint8_t> no_nonces(12 * n, 0);  // unused: the nonce travels in the frame
-    DevRecords d = upload(st, in, out_off, session_table.data()->data(), 32 * K, 32, no_nonces.data(), n);
-    auto [ds, mid] = upload_sessions(st, d, session, K, "wire_open_sessions");
-    auto* macs = (uint8_t*)st.get(S_TAGS, 32 * n);
-    auto* dok = (uint8_t*)st.get(S_OK, n);
-    enet_check(enet_wire_open_batch_sessions(&d.r, ds, (uint32_t)K, mid, macs, dok, st.s()), "wire_open_sessions");
-    st.d2h(ok.data(), dok, n);
-    return download(st, d, out_off);
+    std::vector<std::vector<std::uint8_t>> res;
+    if (n == 0) return res;
+    check_sessions(session, K, "wire_open_sessions");
+    auto j = job_of(enet::hb::Op::WireOpen, frames);
+    j.keys = session_table.data()->data();
+    j.session = session.data();
+    j.n_sessions = (std::uint32_t)K;
+    j.ok_out = ok.data();
+    j.out_vecs = &res;
+    run_host_batch(j);
+    return res;
 }
 
 // ------------------------------------------------------------------------------ proof of work

@@ -1,0 +1,666 @@
+// host_batch.cpp -- the host-memory batch runtime (host_batch.hpp): gather -> device -> scatter
+// over S slots of pinned, device-mapped staging, consecutive chunks overlapped.
+//
+// Reference: the reference seals and opens frames and chunks in host std::vectors
+// (SessionManager.cpp:337-388, 703-854; Message.cpp:305-328; Node.cpp:1414-1417, 1641-1655).
+// crypto::batch::* (Batch.hpp), the FrameQueue flushes and the enet_pipeline_* C ABI all run here.
+#include "host_batch.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "enet_crypto.h"
+
+namespace enet::hb {
+
+namespace {
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("enet host batch: ") + what + ": " + hipGetErrorString(e));
+}
+
+void enet_check(int rc, const char* what) {
+    if (rc != ENET_OK)
+        throw std::runtime_error(std::string("enet host batch: ") + what + ": " + enet_last_error());
+}
+
+// ------------------------------------------------------------------------------ worker pool
+// parallel(parts, fn): fn(0..parts-1) on the pool's threads and the caller, returns when all ran.
+class Pool {
+public:
+    explicit Pool(unsigned workers) {
+        for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void parallel(size_t parts, const std::function<void(size_t)>& fn) {
+        if (parts == 0) return;
+        if (parts == 1 || th_.empty()) {
+            for (size_t i = 0; i < parts; ++i) fn(i);
+            return;
+        }
+        Task t;
+        t.fn = &fn;
+        t.parts = parts;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            task_ = &t;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(t);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [&] { return t.refs == 0 && t.done.load() == t.parts; });
+        task_ = nullptr;
+        lk.unlock();
+        if (t.err) std::rethrow_exception(t.err);
+    }
+
+private:
+    struct Task {
+        const std::function<void(size_t)>* fn = nullptr;
+        size_t parts = 0;
+        std::atomic<size_t> next{0}, done{0};
+        int refs = 0;  // workers inside work() (under mu_)
+        std::exception_ptr err;
+        std::mutex emu;
+    };
+    void work(Task& t) {
+        for (;;) {
+            const size_t i = t.next.fetch_add(1);
+            if (i >= t.parts) break;
+            try {
+                (*t.fn)(i);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(t.emu);
+                if (!t.err) t.err = std::current_exception();
+            }
+            t.done.fetch_add(1);
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || (task_ && gen_ != seen); });
+            if (stop_) return;
+            seen = gen_;
+            Task* t = task_;
+            ++t->refs;
+            lk.unlock();
+            work(*t);
+            lk.lock();
+            if (--t->refs == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    Task* task_ = nullptr;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// ------------------------------------------------------------------------------ buffers
+struct Pinned {  // pinned, device-mapped host memory, grow-only
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        release();
+        const size_t c = std::max<size_t>(n + (n >> 3), 64u << 10);
+        hip_check(hipHostMalloc(reinterpret_cast<void**>(&h), c, hipHostMallocMapped), "hipHostMalloc");
+        void* dp = nullptr;
+        const hipError_t e = hipHostGetDevicePointer(&dp, h, 0);
+        if (e != hipSuccess) {
+            (void)hipHostFree(h);
+            h = nullptr;
+            hip_check(e, "hipHostGetDevicePointer");
+        }
+        d = static_cast<uint8_t*>(dp);
+        cap = c;
+    }
+    void release() {
+        if (h) (void)hipHostFree(h);
+        h = d = nullptr;
+        cap = 0;
+    }
+    ~Pinned() { release(); }
+};
+
+struct DevBuf {  // device memory, grow-only
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    void ensure(size_t n) {
+        if (n <= cap) return;
+        release();
+        const size_t c = std::max<size_t>(n + (n >> 3), 64u << 10);
+        hip_check(hipMalloc(reinterpret_cast<void**>(&p), c), "hipMalloc");
+        cap = c;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    ~DevBuf() { release(); }
+};
+
+// device address of [p, p + n) when the whole range is device-accessible host memory (pinned by
+// hipHostMalloc / registered) or device memory; nullptr for pageable memory
+uint8_t* device_view(const uint8_t* p, uint64_t n) {
+    if (!p || n == 0) return nullptr;
+    auto view = [](const uint8_t* q) -> uint8_t* {
+        hipPointerAttribute_t a{};
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();  // pageable: clear the sticky "invalid value"
+            return nullptr;
+        }
+        if (a.type != hipMemoryTypeHost && a.type != hipMemoryTypeDevice && a.type != hipMemoryTypeManaged)
+            return nullptr;
+        return static_cast<uint8_t*>(a.devicePointer);
+    };
+    uint8_t* a = view(p);
+    uint8_t* b = view(p + (n - 1));
+    if (!a || !b || b - a != (ptrdiff_t)(n - 1)) return nullptr;
+    return a;
+}
+
+int64_t delta_of(Op op) {
+    switch (op) {
+        case Op::FrameSeal: return 32;
+        case Op::FrameOpen: return -32;
+        case Op::WireSeal: return 48;
+        case Op::WireOpen: return -48;
+        default: return 0;
+    }
+}
+
+bool is_open(Op op) {
+    return op == Op::AeadOpen || op == Op::AeadHmacOpen || op == Op::FrameOpen || op == Op::WireOpen ||
+           op == Op::ChunkFetch;
+}
+
+// Small per-record arrays of one chunk, one pinned block: inputs first, outputs last (so SDMA
+// mode moves each half with one copy).
+struct Layout {
+    uint64_t in_off = 0, out_off = 0, keys = 0, nonces = 0, ctr = 0, tags_in = 0, macs_in = 0, ids = 0,
+             session = 0, order = 0, in_end = 0;
+    uint64_t tags_out = 0, macs_out = 0, ok = 0, total = 0;
+    uint64_t key_bytes = 0;
+};
+
+uint64_t up256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+
+Layout layout(const Job& j, uint32_t m) {
+    Layout l;
+    uint64_t at = 0;
+    auto take = [&](uint64_t& where, uint64_t bytes) {
+        where = at;
+        at = up256(at + bytes);
+    };
+    take(l.in_off, 8ull * (m + 1));
+    take(l.out_off, 8ull * (m + 1));
+    l.key_bytes = j.session ? 0 : (j.key_stride ? 32ull * m : 32ull);
+    take(l.keys, std::max<uint64_t>(l.key_bytes, 32));
+    take(l.nonces, 12ull * m);
+    if (j.counters) take(l.ctr, 4ull * m);
+    if (j.tags_in) take(l.tags_in, 16ull * m);
+    if (j.macs_in) take(l.macs_in, 32ull * m);
+    if (j.ids) take(l.ids, 32ull * m);
+    if (j.session) take(l.session, 4ull * m);
+    take(l.order, 4ull * m);
+    l.in_end = at;
+    take(l.tags_out, 16ull * m);
+    take(l.macs_out, 32ull * m);
+    take(l.ok, m);
+    l.total = at;
+    return l;
+}
+
+std::atomic<int> g_mode{-1};
+
+}  // namespace
+
+int64_t out_delta(Op op) { return delta_of(op); }
+
+Mode default_mode() {
+    int m = g_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* e = std::getenv("ENET_HOST_MODE");
+        m = (e && std::strcmp(e, "sdma") == 0) ? (int)Mode::Sdma : (int)Mode::ZeroCopy;
+        g_mode.store(m, std::memory_order_relaxed);
+    }
+    return (Mode)m;
+}
+
+void set_default_mode(Mode m) { g_mode.store((int)m, std::memory_order_relaxed); }
+
+uint32_t worker_threads() {
+    static const uint32_t n = [] {
+        if (const char* e = std::getenv("ENET_HOST_THREADS")) return (uint32_t)std::max(0l, std::strtol(e, nullptr, 10));
+        const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+        return std::min<uint32_t>(8, std::max<uint32_t>(1, hc / 2));
+    }();
+    return n;
+}
+
+// ------------------------------------------------------------------------------ engine
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    Pinned in, out, small;
+    DevBuf d_in, d_out, d_small;
+    // the chunk in flight
+    bool busy = false;
+    size_t c0 = 0, c1 = 0;
+    uint64_t out_b = 0;
+    bool direct_out = false;
+    Layout lay{};
+};
+
+class Engine {
+public:
+    Engine(int dev, const Config& cfg) : dev_(dev), cfg_(cfg) {}
+    ~Engine() {
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(dev_);
+        for (auto& sp : slots_) {
+            Slot& s = *sp;
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+            if (s.done) (void)hipEventDestroy(s.done);
+            if (s.stream) (void)hipStreamDestroy(s.stream);
+        }
+        slots_.clear();
+        table_.release();
+        mid_.release();
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    void run(const Job& j);
+    EngineStats stats() const {
+        std::lock_guard<std::mutex> lk(mu_);
+        return st_;
+    }
+
+private:
+    Mode mode() const { return cfg_.mode >= 0 ? (Mode)cfg_.mode : default_mode(); }
+    void setup_slots(uint32_t S) {
+        while (slots_.size() < S) {
+            slots_.emplace_back(std::make_unique<Slot>());
+            Slot& s = *slots_.back();
+            hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+            hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+        }
+    }
+    Pool& pool() {
+        if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
+        return *pool_;
+    }
+    // byte-balanced parts of the records [a, b): parts of >= min_bytes each, at most workers + 1
+    template <class LenF>
+    std::vector<size_t> split(size_t a, size_t b, uint64_t bytes, LenF len) {
+        const uint64_t min_bytes = 256u << 10;
+        const uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(worker_threads() + 1, bytes / min_bytes));
+        std::vector<size_t> cut{a};
+        uint64_t acc = 0, next = bytes / P;
+        for (size_t i = a; i < b && cut.size() < P; ++i) {
+            acc += len(i);
+            if (acc >= next && i + 1 < b) {
+                cut.push_back(i + 1);
+                next = bytes * cut.size() / P;
+            }
+        }
+        cut.push_back(b);
+        return cut;
+    }
+    void prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b, uint32_t mx);
+    void launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixed);
+    void finish(Slot& s, const Job& j);
+
+    int dev_;
+    Config cfg_;
+    mutable std::mutex mu_;
+    std::vector<std::unique_ptr<Slot>> slots_;
+    std::unique_ptr<Pool> pool_;
+    EngineStats st_{};
+    // per job
+    const uint8_t* in_dev_ = nullptr;   // device view of the caller's input arena (direct in)
+    uint8_t* out_dev_ = nullptr;        // ... output arena (direct out)
+    std::vector<uint64_t> lin_, lout_;  // record lengths in / out
+    DevBuf table_, mid_;                // session key table + HMAC midstates on the device
+    const uint8_t* in_ptr(const Job& j, size_t i) const {
+        return j.in_spans.empty() ? j.in_base + j.in_off[i] : j.in_spans[i].data();
+    }
+};
+
+void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b, uint32_t mx) {
+    const uint32_t m = (uint32_t)(c1 - c0);
+    const Mode md = mode();
+    s.lay = layout(j, m);
+    const Layout& l = s.lay;
+    s.small.ensure(l.total);
+    if (md == Mode::Sdma) {
+        s.d_small.ensure(l.total);
+        s.d_in.ensure(in_b);
+        s.d_out.ensure(out_b);
+    }
+    // ---- inputs: gather the records into the pinned arena (unless the caller's is usable)
+    if (!in_dev_) {
+        s.in.ensure(in_b);
+        uint8_t* base = s.in.h;
+        const auto cut = split(c0, c1, in_b, [&](size_t i) { return lin_[i]; });
+        std::vector<uint64_t> at(cut.size());
+        uint64_t o = 0;
+        for (size_t p = 0, i = c0; p + 1 < cut.size(); ++p) {
+            at[p] = o;
+            for (; i < cut[p + 1]; ++i) o += lin_[i];
+        }
+        pool().parallel(cut.size() - 1, [&](size_t p) {
+            uint64_t w = at[p];
+            for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
+                if (lin_[i]) std::memcpy(base + w, in_ptr(j, i), lin_[i]);
+                w += lin_[i];
+            }
+        });
+        st_.gathered_bytes += in_b;
+    }
+    if (md == Mode::ZeroCopy && !s.direct_out) s.out.ensure(out_b);
+    if (md == Mode::Sdma && !s.direct_out) s.out.ensure(out_b);
+    // ---- small arrays (rebased offsets, keys, nonces, ...)
+    uint8_t* sm = s.small.h;
+    auto* io = reinterpret_cast<uint64_t*>(sm + l.in_off);
+    auto* oo = reinterpret_cast<uint64_t*>(sm + l.out_off);
+    io[0] = oo[0] = 0;
+    for (uint32_t k = 0; k < m; ++k) {
+        io[k + 1] = io[k] + lin_[c0 + k];
+        oo[k + 1] = oo[k] + lout_[c0 + k];
+    }
+    if (!j.session) std::memcpy(sm + l.keys, j.keys + (j.key_stride ? 32ull * c0 : 0ull), l.key_bytes);
+    if (j.nonces) std::memcpy(sm + l.nonces, j.nonces + 12ull * c0, 12ull * m);
+    else std::memset(sm + l.nonces, 0, 12ull * m);
+    if (j.counters) std::memcpy(sm + l.ctr, j.counters + c0, 4ull * m);
+    if (j.tags_in) std::memcpy(sm + l.tags_in, j.tags_in + 16ull * c0, 16ull * m);
+    if (j.macs_in) std::memcpy(sm + l.macs_in, j.macs_in + 32ull * c0, 32ull * m);
+    if (j.ids) std::memcpy(sm + l.ids, j.ids + 32ull * c0, 32ull * m);
+    if (j.session) std::memcpy(sm + l.session, j.session + c0, 4ull * m);
+    // mixed lengths: longest records first, so the serial per-record chains (SHA-256 is one lane
+    // per record) start at once and short records fill in behind them
+    const bool mixed = in_b != (uint64_t)m * mx;
+    if (mixed) {
+        auto* ord = reinterpret_cast<uint32_t*>(sm + l.order);
+        for (uint32_t k = 0; k < m; ++k) ord[k] = k;
+        const uint64_t* len = lin_.data() + c0;
+        std::stable_sort(ord, ord + m, [len](uint32_t a, uint32_t b) { return len[a] > len[b]; });
+    }
+}
+
+void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixed) {
+    const Mode md = mode();
+    const Layout& l = s.lay;
+    const uint32_t m = (uint32_t)(s.c1 - s.c0);
+    hipStream_t st = s.stream;
+    // device addresses of this chunk's arenas and small block
+    const uint8_t* din;
+    uint8_t* dout;
+    uint8_t* sm;
+    const uint8_t* src_in = in_dev_ ? nullptr : s.in.h;
+    if (md == Mode::Sdma) {
+        const uint8_t* h_in = in_dev_ ? in_ptr(j, s.c0) : src_in;
+        if (in_b) hip_check(hipMemcpyAsync(s.d_in.p, h_in, in_b, hipMemcpyHostToDevice, st), "H2D arena");
+        hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
+        din = s.d_in.p;
+        dout = s.d_out.p;
+        sm = s.d_small.p;
+    } else {
+        din = in_dev_ ? in_dev_ + j.in_off[s.c0] : s.in.d;
+        dout = s.direct_out ? out_dev_ + j.out_off[s.c0] : s.out.d;
+        sm = s.small.d;
+    }
+    if (!din) din = sm;  // an all-empty chunk: any valid address
+    if (!dout) dout = sm + l.ok;
+    enet_records r{};
+    r.count = m;
+    r.in_offsets = reinterpret_cast<const uint64_t*>(sm + l.in_off);
+    r.out_offsets = reinterpret_cast<const uint64_t*>(sm + l.out_off);
+    r.in = din;
+    r.out = dout;
+    r.keys = j.session ? table_.p : sm + l.keys;
+    r.key_stride = j.session ? 32 : j.key_stride;
+    r.nonces = sm + l.nonces;
+    r.order = mixed ? reinterpret_cast<const uint32_t*>(sm + l.order) : nullptr;
+    r.total_bytes_hint = in_b;
+    r.max_len_hint = mx;
+    uint8_t* tags_out = sm + l.tags_out;
+    uint8_t* macs_out = sm + l.macs_out;
+    uint8_t* ok = sm + l.ok;
+    const uint8_t* tags_in = j.tags_in ? sm + l.tags_in : nullptr;
+    const uint8_t* macs_in = j.macs_in ? sm + l.macs_in : nullptr;
+    const uint8_t* ids = j.ids ? sm + l.ids : nullptr;
+    const auto* sess = reinterpret_cast<const uint32_t*>(sm + l.session);
+    const auto* mid = reinterpret_cast<const uint32_t*>(mid_.p);
+    switch (j.op) {
+        case Op::Xor:
+            enet_check(enet_chacha20_xor_batch(&r, j.counters ? reinterpret_cast<const uint32_t*>(sm + l.ctr) : nullptr, st),
+                       "chacha20_xor");
+            break;
+        case Op::AeadSeal: enet_check(enet_aead_seal_batch(&r, nullptr, nullptr, tags_out, st), "aead_seal"); break;
+        case Op::AeadOpen: enet_check(enet_aead_open_batch(&r, nullptr, nullptr, tags_in, ok, st), "aead_open"); break;
+        case Op::AeadHmacSeal: enet_check(enet_aead_hmac_seal_batch(&r, tags_out, macs_out, st), "aead_hmac_seal"); break;
+        case Op::AeadHmacOpen:
+            enet_check(enet_aead_hmac_open_batch(&r, tags_in, macs_in, ok, st), "aead_hmac_open");
+            break;
+        case Op::FrameSeal: enet_check(enet_frame_seal_batch(&r, st), "frame_seal"); break;
+        case Op::FrameOpen: enet_check(enet_frame_open_batch(&r, macs_out, ok, st), "frame_open"); break;
+        case Op::WireSeal:
+            if (j.session) enet_check(enet_wire_seal_batch_sessions(&r, sess, j.n_sessions, mid, st), "wire_seal_sessions");
+            else enet_check(enet_wire_seal_batch(&r, st), "wire_seal");
+            break;
+        case Op::WireOpen:
+            if (j.session)
+                enet_check(enet_wire_open_batch_sessions(&r, sess, j.n_sessions, mid, macs_out, ok, st), "wire_open_sessions");
+            else enet_check(enet_wire_open_batch(&r, macs_out, ok, st), "wire_open");
+            break;
+        case Op::ChunkStore: enet_check(enet_chunk_store_batch(&r, ids, macs_out, st), "chunk_store"); break;
+        case Op::ChunkFetch: enet_check(enet_chunk_fetch_batch(&r, ids, macs_in, ok, st), "chunk_fetch"); break;
+    }
+    if (md == Mode::Sdma) {
+        uint8_t* h_out = s.direct_out ? j.out_base + j.out_off[s.c0] : s.out.h;
+        if (s.out_b) hip_check(hipMemcpyAsync(h_out, s.d_out.p, s.out_b, hipMemcpyDeviceToHost, st), "D2H arena");
+        hip_check(hipMemcpyAsync(s.small.h + l.in_end, s.d_small.p + l.in_end, l.total - l.in_end,
+                                 hipMemcpyDeviceToHost, st), "D2H small");
+    }
+    hip_check(hipEventRecord(s.done, st), "hipEventRecord");
+    s.busy = true;
+}
+
+void Engine::finish(Slot& s, const Job& j) {
+    s.busy = false;
+    hip_check(hipEventSynchronize(s.done), "chunk sync");
+    const size_t c0 = s.c0, c1 = s.c1;
+    const uint32_t m = (uint32_t)(c1 - c0);
+    const Layout& l = s.lay;
+    const uint8_t* sm = s.small.h;
+    if (j.tags_out && (j.op == Op::AeadSeal || j.op == Op::AeadHmacSeal))
+        std::memcpy(j.tags_out + 16ull * c0, sm + l.tags_out, 16ull * m);
+    if (j.macs_out && (j.op == Op::AeadHmacSeal || j.op == Op::FrameOpen || j.op == Op::WireOpen || j.op == Op::ChunkStore))
+        std::memcpy(j.macs_out + 32ull * c0, sm + l.macs_out, 32ull * m);
+    if (j.ok_out && is_open(j.op)) std::memcpy(j.ok_out + c0, sm + l.ok, m);
+    if (s.direct_out || s.out_b == 0) {
+        if (j.out_vecs)
+            for (size_t i = c0; i < c1; ++i) (*j.out_vecs)[i].clear();
+        return;
+    }
+    const uint8_t* base = s.out.h;
+    const auto cut = split(c0, c1, s.out_b, [&](size_t i) { return lout_[i]; });
+    std::vector<uint64_t> at(cut.size());
+    uint64_t o = 0;
+    for (size_t p = 0, i = c0; p + 1 < cut.size(); ++p) {
+        at[p] = o;
+        for (; i < cut[p + 1]; ++i) o += lout_[i];
+    }
+    pool().parallel(cut.size() - 1, [&](size_t p) {
+        uint64_t r = at[p];
+        for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
+            const uint64_t len = lout_[i];
+            if (j.out_vecs) {
+                auto& v = (*j.out_vecs)[i];
+                v.resize(len);
+                if (len) std::memcpy(v.data(), base + r, len);
+            } else if (len) {
+                std::memcpy(j.out_base + j.out_off[i], base + r, len);
+            }
+            r += len;
+        }
+    });
+    st_.scattered_bytes += s.out_b;
+}
+
+void Engine::run(const Job& j) {
+    const size_t n = j.n;
+    if (n == 0) return;
+    if (n > 0xFFFFFFFFull) throw std::invalid_argument("enet host batch: more than 2^32 - 1 records");
+    if (!j.in_spans.empty() ? j.in_spans.size() != n : (!j.in_base || !j.in_off))
+        throw std::invalid_argument("enet host batch: input records missing");
+    if (!j.out_vecs && (!j.out_base || !j.out_off)) throw std::invalid_argument("enet host batch: output missing");
+    if (!j.keys) throw std::invalid_argument("enet host batch: keys missing");
+    if (j.key_stride != 0 && j.key_stride != 32) throw std::invalid_argument("enet host batch: key_stride must be 0 or 32");
+    if (!j.nonces && j.op != Op::WireOpen) throw std::invalid_argument("enet host batch: nonces missing");
+    if (j.session && !j.n_sessions) throw std::invalid_argument("enet host batch: empty session table");
+    std::lock_guard<std::mutex> lk(mu_);
+    int prev = -1;
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev_) hip_check(hipSetDevice(dev_), "hipSetDevice");
+    struct Restore {
+        int prev, dev;
+        ~Restore() {
+            if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+        }
+    } restore{prev, dev_};
+
+    const Mode md = mode();
+    const uint32_t S = cfg_.slots ? std::min<uint32_t>(cfg_.slots, 8) : 3u;
+    setup_slots(S);
+    // lengths
+    const int64_t delta = delta_of(j.op);
+    lin_.resize(n);
+    lout_.resize(n);
+    uint64_t in_total = 0, out_total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t a = j.in_spans.empty() ? j.in_off[i + 1] - j.in_off[i] : j.in_spans[i].size();
+        if (j.in_spans.empty() && j.in_off[i + 1] < j.in_off[i])
+            throw std::invalid_argument("enet host batch: input offsets must be non-decreasing");
+        lin_[i] = a;
+        lout_[i] = (uint64_t)std::max<int64_t>(0, (int64_t)a + delta);
+        in_total += a;
+        out_total += lout_[i];
+        if (!j.out_vecs && j.out_off[i + 1] - j.out_off[i] != lout_[i])
+            throw std::invalid_argument("enet host batch: output offsets do not give the op's output lengths");
+    }
+    if (j.out_vecs) j.out_vecs->resize(n);
+    // in place where the caller's arenas are device-accessible
+    in_dev_ = j.in_spans.empty() ? device_view(j.in_base + j.in_off[0], in_total) : nullptr;
+    out_dev_ = j.out_vecs ? nullptr : device_view(j.out_base + j.out_off[0], out_total);
+    if (in_dev_) in_dev_ -= j.in_off[0];
+    if (out_dev_) out_dev_ -= j.out_off[0];
+    const bool direct_out = out_dev_ != nullptr;
+    // sessions: key table and its HMAC midstates on the device, once per job
+    if (j.session) {
+        table_.ensure(32ull * j.n_sessions);
+        mid_.ensure(64ull * j.n_sessions);
+        hipStream_t s0 = slots_[0]->stream;
+        hip_check(hipMemcpyAsync(table_.p, j.keys, 32ull * j.n_sessions, hipMemcpyHostToDevice, s0), "H2D sessions");
+        enet_check(enet_hmac_midstates(table_.p, j.n_sessions, reinterpret_cast<uint32_t*>(mid_.p), s0), "midstates");
+        hip_check(hipStreamSynchronize(s0), "session setup");
+    }
+    // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
+    // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
+    uint64_t chunk = cfg_.chunk_bytes;
+    if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20))
+                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20));
+    st_.jobs += 1;
+    st_.records += n;
+    st_.in_bytes += in_total;
+    st_.out_bytes += out_total;
+    size_t c0 = 0, k = 0;
+    std::exception_ptr err;
+    try {
+        while (c0 < n) {
+            size_t c1 = c0 + 1;
+            uint64_t ib = lin_[c0], ob = lout_[c0];
+            uint32_t mx = (uint32_t)std::min<uint64_t>(lin_[c0], 0xFFFFFFFFu);
+            while (c1 < n && ib + lin_[c1] <= chunk && ob + lout_[c1] <= chunk + (chunk >> 2) && c1 - c0 < (1u << 22)) {
+                ib += lin_[c1];
+                ob += lout_[c1];
+                mx = std::max<uint32_t>(mx, (uint32_t)std::min<uint64_t>(lin_[c1], 0xFFFFFFFFu));
+                ++c1;
+            }
+            Slot& s = *slots_[k % S];
+            ++k;
+            if (s.busy) finish(s, j);
+            s.c0 = c0;
+            s.c1 = c1;
+            s.out_b = ob;
+            s.direct_out = direct_out;
+            prepare(s, j, c0, c1, ib, ob, mx);
+            launch(s, j, ib, mx, ib != (uint64_t)(c1 - c0) * mx);
+            st_.chunks += 1;
+            if (in_dev_) st_.direct_in += 1;
+            if (direct_out) st_.direct_out += 1;
+            c0 = c1;
+        }
+        for (size_t q = 0; q < S; ++q) {
+            Slot& s = *slots_[(k + q) % S];
+            if (s.busy) finish(s, j);
+        }
+    } catch (...) {
+        err = std::current_exception();
+    }
+    if (err) {  // drain whatever is still in flight before the caller's buffers go away
+        for (auto& s : slots_) {
+            if (s->stream) (void)hipStreamSynchronize(s->stream);
+            s->busy = false;
+        }
+        std::rethrow_exception(err);
+    }
+}
+
+// ------------------------------------------------------------------------------ API
+Engine& shared_engine(int dev) {
+    static std::mutex mu;
+    static std::map<int, Engine*>* engines = new std::map<int, Engine*>();  // never destroyed: no HIP at exit
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = engines->find(dev);
+    if (it != engines->end()) return *it->second;
+    Engine* e = new Engine(dev, Config{});
+    (*engines)[dev] = e;
+    return *e;
+}
+
+Engine* create_engine(int dev, const Config& cfg) { return new Engine(dev, cfg); }
+void destroy_engine(Engine* e) { delete e; }
+void run(Engine& e, const Job& job) { e.run(job); }
+EngineStats stats(const Engine& e) { return e.stats(); }
+
+}  // namespace enet::hb

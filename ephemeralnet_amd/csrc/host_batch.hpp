@@ -1,0 +1,104 @@
+// host_batch.hpp -- the host-memory batch runtime: records that start and end in HOST memory
+// (socket / relay buffers, chunk files: SessionManager.cpp:337-388, 703-854; Node.cpp:1414-1417,
+// 1641-1655) through the MI355X kernels, at PCIe rate.
+//
+// One engine per device.  A job (one crypto::batch call, one enet_pipeline_* call) is cut into
+// chunks on record boundaries; every chunk goes through S slots of pinned, device-mapped staging:
+//     gather  (host worker threads: caller records -> the slot's pinned arena, per-record small
+//              arrays rebased into the slot's pinned small block)
+//     device  (one HIP stream per slot: the kernel(s), reading / writing the pinned staging over
+//              PCIe or the device arenas behind SDMA copies -- see Mode)
+//     scatter (host worker threads: the slot's pinned output -> the caller's records / vectors,
+//              small outputs -> the caller's arrays)
+// and the three stages of consecutive chunks overlap.  Inputs and outputs that are already
+// device-accessible (pinned by hipHostMalloc / enet_host_alloc, or registered) skip the
+// gather / scatter copies: the device stage works on them in place.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <span>
+#include <vector>
+
+namespace enet::hb {
+
+enum class Op : int {
+    Xor,           // ChaCha20::apply (counters: start counter per record, nullable = 0)
+    AeadSeal,      // RFC 8439 seal -> tags_out
+    AeadOpen,      // RFC 8439 open (tags_in) -> ok_out
+    AeadHmacSeal,  // C5: AEAD + HMAC-SHA256(key, pt) -> tags_out, macs_out
+    AeadHmacOpen,  // C5 open: tags_in, macs_in -> ok_out
+    FrameSeal,     // body = ChaCha20_{K,N,0}(m || HMAC_K(m)); |out| = |in| + 32
+    FrameOpen,     // -> macs_out (nullable), ok_out; |out| = |in| - 32
+    WireSeal,      // nonce || BE32 || body; |out| = |in| + 48
+    WireOpen,      // nonce from the frame -> ok_out; |out| = |in| - 48
+    ChunkStore,    // ChaCha20 from LE32(id) + SHA-256(pt) -> macs_out (chunk hashes); ids given
+    ChunkFetch,    // decrypt + SHA-256 check against macs_in -> ok_out
+};
+
+// |out_i| as a function of |in_i|
+int64_t out_delta(Op op);
+
+struct Job {
+    Op op = Op::Xor;
+    size_t n = 0;
+    // input record i: in_spans[i] when in_spans is non-empty, else in_base[in_off[i] .. in_off[i+1])
+    std::span<const std::span<const uint8_t>> in_spans;
+    const uint8_t* in_base = nullptr;
+    const uint64_t* in_off = nullptr;
+    // output record i (|out_i| = max(0, |in_i| + out_delta(op))): out_vecs[i] (resized here) when
+    // set, else out_base[out_off[i] .. out_off[i+1]) (the caller's offsets must give that length)
+    std::vector<std::vector<uint8_t>>* out_vecs = nullptr;
+    uint8_t* out_base = nullptr;
+    const uint64_t* out_off = nullptr;
+    // per-record small inputs (host memory)
+    const uint8_t* keys = nullptr;      // [n][32]; [1][32] when key_stride == 0; the table for sessions
+    uint32_t key_stride = 32;
+    const uint8_t* nonces = nullptr;    // [n][12] (WireOpen: unused)
+    const uint32_t* counters = nullptr; // Xor: [n] start counters, nullable
+    const uint8_t* tags_in = nullptr;   // [n][16]
+    const uint8_t* macs_in = nullptr;   // [n][32]: AeadHmacOpen MACs, ChunkFetch expected hashes
+    const uint8_t* ids = nullptr;       // [n][32]: chunk ids (ChunkStore / ChunkFetch)
+    // session-keyed frames (WireSeal / WireOpen): keys is a table of n_sessions keys
+    const uint32_t* session = nullptr;
+    uint32_t n_sessions = 0;
+    // per-record small outputs (host memory, nullable where the op allows)
+    uint8_t* tags_out = nullptr;        // [n][16]
+    uint8_t* macs_out = nullptr;        // [n][32]
+    uint8_t* ok_out = nullptr;          // [n]
+};
+
+// How the device stage moves the bytes (ENET_HOST_MODE=zc|sdma; enet_host_set_mode):
+//   ZeroCopy -- the kernels read the pinned input and write the pinned output directly over PCIe
+//               (no DMA, no device arenas); both directions move at once inside one launch
+//   Sdma     -- H2D copy into a device arena, kernel, D2H copy back (the copy engines)
+enum class Mode : int { ZeroCopy = 0, Sdma = 1 };
+
+struct Config {
+    uint64_t chunk_bytes = 0;  // 0: the mode's default
+    uint32_t slots = 0;        // 0: the mode's default
+    int mode = -1;             // -1: process default (env / enet_host_set_mode)
+};
+
+class Engine;
+// The engine of device `dev` shared by the crypto::batch calls of the whole process (created on
+// first use; calls are serialised per device).
+Engine& shared_engine(int dev);
+Engine* create_engine(int dev, const Config& cfg);
+void destroy_engine(Engine* e);
+// Runs the job to completion; throws std::invalid_argument / std::runtime_error / std::bad_alloc.
+void run(Engine& e, const Job& job);
+
+Mode default_mode();
+void set_default_mode(Mode m);
+// host worker threads that gather / scatter (ENET_HOST_THREADS; default min(8, CPUs / 2))
+uint32_t worker_threads();
+
+struct EngineStats {
+    uint64_t jobs = 0, chunks = 0, records = 0, in_bytes = 0, out_bytes = 0;
+    uint64_t gathered_bytes = 0, scattered_bytes = 0;  // copied by the host workers
+    uint64_t direct_in = 0, direct_out = 0;             // chunks whose side ran in place
+};
+EngineStats stats(const Engine& e);
+
+}  // namespace enet::hb

@@ -213,13 +213,14 @@ ENET_API int enet_session_key_batch(uint32_t n, const uint8_t* secrets, const ui
  * SessionManager.cpp:362-387 and 815-822; chunk files, Node.cpp:1414-1417 and 1641-1655).  These
  * calls take an enet_records batch whose arenas, offsets, keys, nonces, counters, tags, MACs and
  * ok flags are all HOST pointers, cut it into chunks of about `chunk_bytes` on record boundaries
- * and run H2D -> kernel(s) -> D2H per chunk on `streams` HIP streams, so copies of one chunk
- * overlap the kernels and copies of the others; inside a chunk of mixed lengths records are run
- * longest first.  Arenas from enet_host_alloc (pinned) move by
- * asynchronous DMA; pageable arenas work but each of their copies blocks the calling thread.
- * Records keep their length (in/out offsets describe equal-length records); `order` must be
- * NULL.  Every call blocks until all outputs are in host memory.  A pipeline owns its streams
- * and device / pinned staging buffers (grown on demand) and serves one host thread at a time. */
+ * and run each chunk through one of `streams` slots (a HIP stream plus pinned, device-mapped
+ * staging), chunks overlapped; inside a chunk of mixed lengths records are run longest first.
+ * Arenas the device can address (enet_host_alloc, hipHostMalloc, registered memory) are worked
+ * on in place; pageable arenas are gathered into / scattered out of the pinned staging by the
+ * runtime's host worker threads (ENET_HOST_THREADS).  See enet_host_set_mode for how the
+ * kernels reach host memory.  `order` must be NULL.  Every call blocks until all outputs are in
+ * host memory.  A pipeline owns its streams and staging (grown on demand) and serves one host
+ * thread at a time. */
 typedef struct enet_pipeline enet_pipeline;
 /* device: HIP ordinal; chunk_bytes: 0 = 16 MiB (mixed-length batches with HMAC want larger
  * chunks: one lane hashes a whole record, so a chunk takes at least its longest record's
@@ -240,6 +241,16 @@ ENET_API int enet_pipeline_aead_hmac_seal(enet_pipeline* pipe, const enet_record
                                           uint8_t* tags, uint8_t* macs);
 ENET_API int enet_pipeline_aead_hmac_open(enet_pipeline* pipe, const enet_records* host_records,
                                           const uint8_t* tags, const uint8_t* macs, uint8_t* ok);
+/* Whole wire frames (enet_wire_seal_batch / enet_wire_open_batch) from and to host memory:
+ * seal out_offsets give |m_i| + 48, open out_offsets give max(0, |f_i| - 48); ok [n]. */
+ENET_API int enet_pipeline_wire_seal(enet_pipeline* pipe, const enet_records* host_records);
+ENET_API int enet_pipeline_wire_open(enet_pipeline* pipe, const enet_records* host_records, uint8_t* ok);
+/* How host-resident batches reach the kernels (pipelines and crypto::batch::*), process-wide:
+ * 0 = zero-copy -- the kernels read and write pinned host memory directly over PCIe (the
+ * default); 1 = SDMA -- H2D copy, kernel, D2H copy per chunk.  ENET_HOST_MODE=zc|sdma sets the
+ * initial value.  Results are identical. */
+ENET_API int enet_host_set_mode(int mode);
+ENET_API int enet_host_mode(void);
 /* ---- several devices of one node (no reference counterpart -- the reference
  *      runs src/crypto on one core per call): one pipeline, host thread and stream set per device,
  *      each call cuts the batch into contiguous record ranges balanced by input bytes and runs

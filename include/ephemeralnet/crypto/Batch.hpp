@@ -1,7 +1,7 @@
 // Batch.hpp -- crypto::batch: the many-records-per-call form of the reference API, for callers
 // that collect work across sessions / chunks (batched session-frame codec, store
-// pipeline).  Host vectors in, host vectors out; one H2D, one kernel sequence and one D2H per
-// call.  Device-resident callers use the C ABI (enet_crypto.h) directly.
+// pipeline).  Host memory in, host memory out (see below).  Device-resident callers use the C ABI
+// (enet_crypto.h) directly.
 #pragma once
 
 #include <array>
@@ -22,10 +22,23 @@ struct Sealed {
     std::array<std::uint8_t, 16> tag{};
 };
 
+// Every call below takes host memory and runs on the MI355X of the calling thread's device
+// through the host-memory batch runtime: the records are gathered by host worker threads into
+// pinned, device-mapped staging, chunk by chunk, while earlier chunks run on the device and
+// later results are scattered back -- never a pageable hipMemcpy.  Outputs come either as one
+// vector per record (the reference's own shape) or, for throughput, written into ONE
+// caller-provided contiguous span: record i at packed_offsets(inputs, delta)[i], where delta is
+// the op's length change (0 cipher / AEAD, +48 wire seal, -48 wire open, clamped at 0).
+ENET_CXX_API std::vector<std::uint64_t> packed_offsets(std::span<const std::span<const std::uint8_t>> records,
+                                                       std::int64_t delta);
+
 // ChaCha20::apply for many records (counters[i] = start counter; empty span = all 0).
 ENET_CXX_API std::vector<std::vector<std::uint8_t>> chacha20_apply(
     std::span<const Key> keys, std::span<const Nonce> nonces,
     std::span<const std::span<const std::uint8_t>> inputs, std::span<const std::uint32_t> counters);
+ENET_CXX_API void chacha20_apply(std::span<const Key> keys, std::span<const Nonce> nonces,
+                                 std::span<const std::span<const std::uint8_t>> inputs,
+                                 std::span<const std::uint32_t> counters, std::span<std::uint8_t> out);
 
 // RFC 8439 ChaCha20-Poly1305 (no AAD) for many records.
 ENET_CXX_API std::vector<Sealed> aead_seal(std::span<const Key> keys,
@@ -36,6 +49,15 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> aead_open(
     std::span<const Key> keys, std::span<const Nonce> nonces,
     std::span<const std::span<const std::uint8_t>> ciphertexts,
     std::span<const std::array<std::uint8_t, 16>> tags, std::vector<std::uint8_t>& ok);
+// contiguous forms: ciphertexts / plaintexts packed into `out` (packed_offsets(.., 0)), tags[i],
+// ok[i] (a failed record's plaintext is zeroed)
+ENET_CXX_API void aead_seal(std::span<const Key> keys, std::span<const Nonce> nonces,
+                            std::span<const std::span<const std::uint8_t>> plaintexts, std::span<std::uint8_t> out,
+                            std::span<std::array<std::uint8_t, 16>> tags);
+ENET_CXX_API void aead_open(std::span<const Key> keys, std::span<const Nonce> nonces,
+                            std::span<const std::span<const std::uint8_t>> ciphertexts,
+                            std::span<const std::array<std::uint8_t, 16>> tags, std::span<std::uint8_t> out,
+                            std::span<std::uint8_t> ok);
 
 // SHA-256 digests of many messages (Sha256::digest).
 ENET_CXX_API std::vector<std::array<std::uint8_t, 32>> sha256(
@@ -77,6 +99,14 @@ ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_seal(
 ENET_CXX_API std::vector<std::vector<std::uint8_t>> wire_open(
     std::span<const std::array<std::uint8_t, 32>> session_keys,
     std::span<const std::span<const std::uint8_t>> frames, std::vector<std::uint8_t>& ok);
+// contiguous forms: frames packed into `frames` (packed_offsets(messages, 48)); messages packed
+// into `messages` (packed_offsets(frames, -48)), ok[i] (a failed message is zeroed)
+ENET_CXX_API void wire_seal(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                            std::span<const Nonce> nonces, std::span<const std::span<const std::uint8_t>> messages,
+                            std::span<std::uint8_t> frames);
+ENET_CXX_API void wire_open(std::span<const std::array<std::uint8_t, 32>> session_keys,
+                            std::span<const std::span<const std::uint8_t>> frames, std::span<std::uint8_t> messages,
+                            std::span<std::uint8_t> ok);
 // The same frames from a table of session keys: frame i belongs to session_table[session[i]]
 // (bytes identical to wire_seal / wire_open with session_keys[i] = session_table[session[i]]).
 // The HMAC key-block midstates are computed once per table entry on the device

@@ -297,6 +297,74 @@ int main() {
             std::vector<uint8_t> buf = unhex(p);
             crypto::ChaCha20::apply(key, nonce, buf, buf, (uint32_t)std::stoul(c));
             std::cout << hex(buf) << "\n";
+        } else if (op == "packed") {
+            // the contiguous-output batch overloads: AEAD seal / open and wire
+            // seal / open of n records written into ONE output span each, plus the vector forms of
+            // the same calls for comparison.  Tampered: AEAD tag of record 1, wire body of record 2.
+            // Prints: ct tags aead_ok pt frames wire_ok msgs same(vector forms equal packed)
+            size_t n = 0; in >> n;
+            std::vector<crypto::Key> keys(n);
+            std::vector<std::array<uint8_t, 32>> wkeys(n);
+            std::vector<crypto::Nonce> nonces(n);
+            std::vector<std::vector<uint8_t>> msgs(n);
+            for (size_t i = 0; i < n; ++i) {
+                std::string k, nn, m; in >> k >> nn >> m;
+                auto kb = unhex(k), nb = unhex(nn);
+                std::copy(kb.begin(), kb.end(), keys[i].bytes.begin());
+                std::copy(kb.begin(), kb.end(), wkeys[i].begin());
+                std::copy(nb.begin(), nb.end(), nonces[i].bytes.begin());
+                msgs[i] = unhex(m);
+            }
+            std::vector<std::span<const uint8_t>> ms(msgs.begin(), msgs.end());
+            namespace B = crypto::batch;
+            const auto off0 = B::packed_offsets(ms, 0), off48 = B::packed_offsets(ms, 48);
+            std::vector<uint8_t> ct(off0.back()), pt(off0.back()), aok(n), frames(off48.back()), wok(n);
+            std::vector<std::array<uint8_t, 16>> tags(n);
+            B::aead_seal(keys, nonces, ms, ct, tags);
+            std::vector<std::span<const uint8_t>> cs(n);
+            for (size_t i = 0; i < n; ++i) cs[i] = std::span<const uint8_t>(ct.data() + off0[i], off0[i + 1] - off0[i]);
+            auto bad = tags;
+            if (n > 1) bad[1][3] ^= 1;
+            std::fill(pt.begin(), pt.end(), 0xEE);
+            B::aead_open(keys, nonces, cs, bad, pt, aok);
+            B::wire_seal(wkeys, nonces, ms, frames);
+            auto fr2 = frames;
+            if (n > 2) fr2[off48[2] + 20] ^= 0x40;
+            std::vector<std::span<const uint8_t>> fs(n);
+            for (size_t i = 0; i < n; ++i) fs[i] = std::span<const uint8_t>(fr2.data() + off48[i], off48[i + 1] - off48[i]);
+            const auto offm = B::packed_offsets(fs, -48);
+            std::vector<uint8_t> back(offm.back(), 0xEE);
+            B::wire_open(wkeys, fs, back, wok);
+            // the vector forms give the same bytes
+            bool same = true;
+            auto sv = B::aead_seal(keys, nonces, ms);
+            for (size_t i = 0; i < n; ++i)
+                same = same && sv[i].tag == tags[i] &&
+                       std::equal(sv[i].data.begin(), sv[i].data.end(), ct.begin() + (ptrdiff_t)off0[i]);
+            std::vector<uint8_t> vok;
+            auto pv = B::aead_open(keys, nonces, cs, bad, vok);
+            for (size_t i = 0; i < n; ++i)
+                same = same && vok[i] == aok[i] && std::equal(pv[i].begin(), pv[i].end(), pt.begin() + (ptrdiff_t)off0[i]);
+            auto wv = B::wire_seal(wkeys, nonces, ms);
+            for (size_t i = 0; i < n; ++i)
+                same = same && std::equal(wv[i].begin(), wv[i].end(), frames.begin() + (ptrdiff_t)off48[i]);
+            std::vector<uint8_t> cc(off0.back());
+            B::chacha20_apply(keys, nonces, ms, {}, cc);
+            auto cv = B::chacha20_apply(keys, nonces, ms, {});
+            for (size_t i = 0; i < n; ++i) {
+                std::vector<uint8_t> one;
+                crypto::ChaCha20::apply(keys[i], nonces[i], msgs[i], one, 0);
+                same = same && cv[i] == one && std::equal(one.begin(), one.end(), cc.begin() + (ptrdiff_t)off0[i]);
+            }
+            std::string ao, wo;
+            for (size_t i = 0; i < n; ++i) {
+                ao += aok[i] ? '1' : '0';
+                wo += wok[i] ? '1' : '0';
+            }
+            std::vector<uint8_t> tg;
+            for (auto& t : tags) tg.insert(tg.end(), t.begin(), t.end());
+            std::cout << hex(ct) << " " << hex(tg) << " " << ao << " " << hex(pt) << " " << hex(frames) << " " << wo
+                      << " " << hex(back) << " " << (same ? "1" : "0") << "\n";
         } else if (op == "fork_nonces") {
             // the frame nonce generator after fork(): parent and child each seal one frame (host
             // engine, FrameQueue::seal) from a generator that was in use before the fork; the

@@ -135,6 +135,44 @@ def test_cpp_scalar_api_device_failure_finishes_on_host(api_bin, golden):
     assert err.count("finished on the host engine") == 1
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,maxlen,seed", [(1, 100, 1), (37, 3000, 2), (300, 1600, 3), (12, 70000, 4)])
+def test_cpp_packed_batch_overloads_vs_oracle(api_bin, n, maxlen, seed):
+    """The contiguous-output forms of crypto::batch::aead_seal / aead_open / wire_seal / wire_open /
+    chacha20_apply (host std::vector records in, ONE packed output span) through the host-memory
+    batch runtime: bit-exact with the oracle record by record, a tampered tag / frame rejected and
+    zeroed, and equal to the vector-per-record forms of the same calls."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    lens = [int(x) for x in rng.integers(0, maxlen + 1, n)]
+    lens[: min(n, 4)] = [0, 1, 64, maxlen][: min(n, 4)]
+    keys = [splitmix_bytes(1000 * seed + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(2000 * seed + i, 12) for i in range(n)]
+    msgs = [splitmix_bytes(3000 * seed + i, L) for i, L in enumerate(lens)]
+    line = f"packed {n} " + " ".join(f"{k.hex()} {v.hex()} {h(m)}" for k, v, m in zip(keys, nonces, msgs))
+    res, err = run_ops(api_bin, [line])
+    ct, tags, aok, pt, frames, wok, back, same = res[0].split()
+    unhex = lambda x: b"" if x == "-" else bytes.fromhex(x)
+    ct, tags, pt, frames, back = map(unhex, (ct, tags, pt, frames, back))
+    assert same == "1"
+    o = 0
+    fo = 0
+    want_ct, want_fr = b"", b""
+    for i in range(n):
+        c, t = oracle.aead_seal(keys[i], nonces[i], msgs[i])
+        assert ct[o:o + lens[i]] == c and tags[16 * i:16 * i + 16] == t, i
+        body = oracle.frame_seal(keys[i], nonces[i], msgs[i])
+        wire = nonces[i] + (len(body)).to_bytes(4, "big") + body
+        assert frames[fo:fo + len(wire)] == wire, i
+        bad_a, bad_w = i == 1, i == 2
+        assert aok[i] == ("0" if bad_a else "1") and wok[i] == ("0" if bad_w else "1"), i
+        assert pt[o:o + lens[i]] == (bytes(lens[i]) if bad_a else msgs[i]), i
+        assert back[o:o + lens[i]] == (bytes(lens[i]) if bad_w else msgs[i]), i
+        o += lens[i]
+        fo += len(wire)
+    assert len(ct) == o and len(frames) == fo
+
+
 def test_cpp_frame_nonces_differ_after_fork(api_bin):
     """the per-thread frame-nonce generator is copied by fork(); a pthread_atfork
     handler makes the child re-key, so parent and child never hand out the same nonce (the

@@ -1,0 +1,289 @@
+// batch_bench.cpp -- host-memory throughput of the C++ batch API (include/ephemeralnet/crypto/
+// Batch.hpp) against the pinned C-ABI pipeline (enet_pipeline_*) on the same shapes.
+//
+//   C2 AEAD : 65 536 x 4 KiB, batch::aead_seal + aead_open from std::vector records
+//   C3 wire : 1 M x 1 500 B messages, batch::wire_seal + wire_open (1 548-byte frames)
+// Each shape runs three ways: (a) vector per record in and out (the reference's own shape),
+// (b) vectors in, one contiguous output (the packed overloads), (c) the pinned pipeline with
+// enet_host_alloc arenas (the ceiling the batch API is held to).  Every round trip is checked
+// (every record back, every tag / MAC verified).  One JSON line per case; GiB/s = sum of
+// plaintext bytes / (t_seal + t_open).
+//
+// build: hipcc --offload-arch=gfx950 -O2 -std=c++20 -Iinclude tools/batch_bench.cpp
+//        -Lephemeralnet_amd -lenet_crypto -Wl,-rpath,'$ORIGIN/../ephemeralnet_amd' -o tools/batch_bench
+// usage: batch_bench [c2|c3|all] [reps]
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "enet_crypto.h"
+#include "ephemeralnet/crypto/Batch.hpp"
+
+using namespace ephemeralnet::crypto;
+
+namespace {
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void fill(std::mt19937_64& g, uint8_t* p, size_t n) {
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const uint64_t x = g();
+        std::memcpy(p + i, &x, 8);
+    }
+    for (; i < n; ++i) p[i] = (uint8_t)g();
+}
+
+[[noreturn]] void die(const char* what) {
+    std::fprintf(stderr, "batch_bench: %s\n", what);
+    std::exit(3);
+}
+
+void report(const char* shape, const char* path, size_t n, size_t L, double seal_s, double open_s, int reps) {
+    const double gib = (double)n * L * reps / (1ull << 30);
+    std::printf("{\"shape\":\"%s\",\"path\":\"%s\",\"records\":%zu,\"record_bytes\":%zu,\"reps\":%d,"
+                "\"seal_GiBs\":%.2f,\"open_GiBs\":%.2f,\"seal_open_GiBs\":%.2f}\n",
+                shape, path, n, L, reps, gib / seal_s, gib / open_s, gib / (seal_s + open_s));
+    std::fflush(stdout);
+}
+
+void c2(int reps) {
+    const size_t n = 65536, L = 4096;
+    std::mt19937_64 g(2);
+    std::vector<Key> keys(n);
+    std::vector<Nonce> nonces(n);
+    for (auto& k : keys) fill(g, k.bytes.data(), 32);
+    for (auto& v : nonces) fill(g, v.bytes.data(), 12);
+    std::vector<std::vector<uint8_t>> pt(n, std::vector<uint8_t>(L));
+    for (auto& v : pt) fill(g, v.data(), L);
+    std::vector<std::span<const uint8_t>> ps(pt.begin(), pt.end());
+    // (a) vectors in, vectors out
+    {
+        std::vector<batch::Sealed> sealed;
+        std::vector<std::vector<uint8_t>> back;
+        std::vector<uint8_t> ok;
+        double ts = 0, to = 0;
+        for (int r = -1; r < reps; ++r) {
+            double t0 = now();
+            sealed = batch::aead_seal(keys, nonces, ps);
+            double t1 = now();
+            std::vector<std::span<const uint8_t>> cs(n);
+            std::vector<std::array<uint8_t, 16>> tags(n);
+            for (size_t i = 0; i < n; ++i) {
+                cs[i] = sealed[i].data;
+                tags[i] = sealed[i].tag;
+            }
+            double t2 = now();
+            back = batch::aead_open(keys, nonces, cs, tags, ok);
+            double t3 = now();
+            if (r >= 0) {
+                ts += t1 - t0;
+                to += t3 - t2;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i] || back[i] != pt[i]) die("C2 vectors: round trip failed");
+        report("C2", "batch vectors (std::vector per record in and out)", n, L, ts, to, reps);
+    }
+    // (b) vectors in, packed out
+    {
+        std::vector<uint8_t> ct(n * L), back(n * L), ok(n);
+        std::vector<std::array<uint8_t, 16>> tags(n);
+        std::vector<std::span<const uint8_t>> cs(n);
+        for (size_t i = 0; i < n; ++i) cs[i] = std::span<const uint8_t>(ct.data() + i * L, L);
+        double ts = 0, to = 0;
+        for (int r = -1; r < reps; ++r) {
+            double t0 = now();
+            batch::aead_seal(keys, nonces, ps, ct, tags);
+            double t1 = now();
+            batch::aead_open(keys, nonces, cs, tags, back, ok);
+            double t2 = now();
+            if (r >= 0) {
+                ts += t1 - t0;
+                to += t2 - t1;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i] || std::memcmp(back.data() + i * L, pt[i].data(), L)) die("C2 packed: round trip failed");
+        report("C2", "batch packed (std::vector records in, one contiguous output)", n, L, ts, to, reps);
+    }
+    // (c) pinned pipeline
+    {
+        auto* in = (uint8_t*)enet_host_alloc(n * L);
+        auto* ct = (uint8_t*)enet_host_alloc(n * L);
+        auto* back = (uint8_t*)enet_host_alloc(n * L);
+        auto* tags = (uint8_t*)enet_host_alloc(16 * n);
+        auto* ok = (uint8_t*)enet_host_alloc(n);
+        auto* off = (uint64_t*)enet_host_alloc(8 * (n + 1));
+        auto* kk = (uint8_t*)enet_host_alloc(32 * n);
+        auto* nn = (uint8_t*)enet_host_alloc(12 * n);
+        if (!in || !ct || !back || !tags || !ok || !off || !kk || !nn) die("enet_host_alloc");
+        for (size_t i = 0; i < n; ++i) {
+            std::memcpy(in + i * L, pt[i].data(), L);
+            std::memcpy(kk + 32 * i, keys[i].bytes.data(), 32);
+            std::memcpy(nn + 12 * i, nonces[i].bytes.data(), 12);
+        }
+        for (size_t i = 0; i <= n; ++i) off[i] = i * L;
+        enet_pipeline* p = enet_pipeline_create(0, 0, 0);
+        if (!p) die(enet_last_error());
+        enet_records r{};
+        r.count = (uint32_t)n;
+        r.in_offsets = r.out_offsets = off;
+        r.keys = kk;
+        r.key_stride = 32;
+        r.nonces = nn;
+        r.total_bytes_hint = n * L;
+        r.max_len_hint = (uint32_t)L;
+        double ts = 0, to = 0;
+        for (int k = -1; k < reps; ++k) {
+            r.in = in;
+            r.out = ct;
+            double t0 = now();
+            if (enet_pipeline_aead_seal(p, &r, tags)) die(enet_last_error());
+            double t1 = now();
+            r.in = ct;
+            r.out = back;
+            if (enet_pipeline_aead_open(p, &r, tags, ok)) die(enet_last_error());
+            double t2 = now();
+            if (k >= 0) {
+                ts += t1 - t0;
+                to += t2 - t1;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i]) die("C2 pipeline: tag failed");
+        if (std::memcmp(back, in, n * L)) die("C2 pipeline: round trip failed");
+        report("C2", "pinned pipeline (enet_pipeline_aead_*, enet_host_alloc arenas)", n, L, ts, to, reps);
+        enet_pipeline_destroy(p);
+        for (void* q : {(void*)in, (void*)ct, (void*)back, (void*)tags, (void*)ok, (void*)off, (void*)kk, (void*)nn})
+            enet_host_free(q);
+    }
+}
+
+void c3(int reps) {
+    const size_t n = 1u << 20, L = 1500, F = L + 48;
+    std::mt19937_64 g(3);
+    std::vector<std::array<uint8_t, 32>> keys(n);
+    std::vector<Nonce> nonces(n);
+    for (auto& k : keys) fill(g, k.data(), 32);
+    for (auto& v : nonces) fill(g, v.bytes.data(), 12);
+    std::vector<std::vector<uint8_t>> msg(n, std::vector<uint8_t>(L));
+    for (auto& v : msg) fill(g, v.data(), L);
+    std::vector<std::span<const uint8_t>> ms(msg.begin(), msg.end());
+    {
+        std::vector<std::vector<uint8_t>> frames, back;
+        std::vector<uint8_t> ok;
+        double ts = 0, to = 0;
+        for (int r = -1; r < reps; ++r) {
+            double t0 = now();
+            frames = batch::wire_seal(keys, nonces, ms);
+            double t1 = now();
+            std::vector<std::span<const uint8_t>> fs(frames.begin(), frames.end());
+            double t2 = now();
+            back = batch::wire_open(keys, fs, ok);
+            double t3 = now();
+            if (r >= 0) {
+                ts += t1 - t0;
+                to += t3 - t2;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i] || back[i] != msg[i]) die("C3 vectors: round trip failed");
+        report("C3 wire", "batch vectors (std::vector per record in and out)", n, L, ts, to, reps);
+    }
+    {
+        std::vector<uint8_t> frames(n * F), back(n * L), ok(n);
+        std::vector<std::span<const uint8_t>> fs(n);
+        for (size_t i = 0; i < n; ++i) fs[i] = std::span<const uint8_t>(frames.data() + i * F, F);
+        double ts = 0, to = 0;
+        for (int r = -1; r < reps; ++r) {
+            double t0 = now();
+            batch::wire_seal(keys, nonces, ms, frames);
+            double t1 = now();
+            batch::wire_open(keys, fs, back, ok);
+            double t2 = now();
+            if (r >= 0) {
+                ts += t1 - t0;
+                to += t2 - t1;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i] || std::memcmp(back.data() + i * L, msg[i].data(), L)) die("C3 packed: round trip failed");
+        report("C3 wire", "batch packed (std::vector records in, one contiguous output)", n, L, ts, to, reps);
+    }
+    {
+        auto* in = (uint8_t*)enet_host_alloc(n * L);
+        auto* fr = (uint8_t*)enet_host_alloc(n * F);
+        auto* back = (uint8_t*)enet_host_alloc(n * L);
+        auto* ok = (uint8_t*)enet_host_alloc(n);
+        auto* moff = (uint64_t*)enet_host_alloc(8 * (n + 1));
+        auto* foff = (uint64_t*)enet_host_alloc(8 * (n + 1));
+        auto* kk = (uint8_t*)enet_host_alloc(32 * n);
+        auto* nn = (uint8_t*)enet_host_alloc(12 * n);
+        if (!in || !fr || !back || !ok || !moff || !foff || !kk || !nn) die("enet_host_alloc");
+        for (size_t i = 0; i < n; ++i) {
+            std::memcpy(in + i * L, msg[i].data(), L);
+            std::memcpy(kk + 32 * i, keys[i].data(), 32);
+            std::memcpy(nn + 12 * i, nonces[i].bytes.data(), 12);
+        }
+        for (size_t i = 0; i <= n; ++i) {
+            moff[i] = i * L;
+            foff[i] = i * F;
+        }
+        enet_pipeline* p = enet_pipeline_create(0, 0, 0);
+        if (!p) die(enet_last_error());
+        enet_records s{}, o{};
+        s.count = o.count = (uint32_t)n;
+        s.in_offsets = moff;
+        s.out_offsets = foff;
+        s.in = in;
+        s.out = fr;
+        s.keys = o.keys = kk;
+        s.key_stride = o.key_stride = 32;
+        s.nonces = nn;
+        s.total_bytes_hint = n * L;
+        s.max_len_hint = (uint32_t)L;
+        o.in_offsets = foff;
+        o.out_offsets = moff;
+        o.in = fr;
+        o.out = back;
+        o.nonces = nn;
+        o.total_bytes_hint = n * F;
+        o.max_len_hint = (uint32_t)F;
+        double ts = 0, to = 0;
+        for (int k = -1; k < reps; ++k) {
+            double t0 = now();
+            if (enet_pipeline_wire_seal(p, &s)) die(enet_last_error());
+            double t1 = now();
+            if (enet_pipeline_wire_open(p, &o, ok)) die(enet_last_error());
+            double t2 = now();
+            if (k >= 0) {
+                ts += t1 - t0;
+                to += t2 - t1;
+            }
+        }
+        for (size_t i = 0; i < n; ++i)
+            if (!ok[i]) die("C3 pipeline: MAC failed");
+        if (std::memcmp(back, in, n * L)) die("C3 pipeline: round trip failed");
+        report("C3 wire", "pinned pipeline (enet_pipeline_wire_*, enet_host_alloc arenas)", n, L, ts, to, reps);
+        enet_pipeline_destroy(p);
+        for (void* q : {(void*)in, (void*)fr, (void*)back, (void*)ok, (void*)moff, (void*)foff, (void*)kk, (void*)nn})
+            enet_host_free(q);
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const std::string which = argc > 1 ? argv[1] : "all";
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
+    if (which == "all" || which == "c2") c2(reps);
+    if (which == "all" || which == "c3") c3(reps);
+    return 0;
+}
