@@ -1,13 +1,17 @@
 // frame_queue.cpp -- the cross-session frame queues of Batch.hpp.
 //
-// Many session threads each submit one frame and block.  The queue's worker thread takes what is
-// queued (up to max_frames / max_bytes; with a positive max_delay it first waits for a size limit
-// or the deadline), runs ONE batched pass -- crypto::batch::wire_seal / wire_open on the MI355X --
-// writes every caller's result into that caller's request and wakes exactly those callers;
-// frames arriving meanwhile form the next batch (group commit).  Under the auto and host policies there is no queue: each thread seals / opens its own
-// frame on the host engine, which measured faster than a device pass for MTU frames (see seal()).  A request is owned by the thread that
-// submitted it (it lives on that thread's stack until `done`), results are matched by request,
-// never by position in some shared buffer, so sessions cannot see each other's frames.
+// Session threads submit frames -- blocking (seal / open: the thread sleeps until its frame is
+// done) or not (seal_async / open_async: a future).  Under the device policy the queue's worker
+// threads (max_inflight of them, each with its own host-batch engine: pinned staging and a HIP
+// stream) take what is queued (up to max_frames / max_bytes; with a positive max_delay they first
+// wait for a size limit or the deadline), run ONE batched pass over it on the MI355X, write every
+// request's result into that request and wake / fulfil exactly those requests; frames arriving
+// meanwhile go to the next free worker (group commit, several passes in flight).  Under the auto
+// and host policies there is no queue: each thread seals / opens its own frame on the host engine,
+// which measured faster than a device pass for MTU frames (see seal()).  A request is owned by its
+// submitter (a blocking one lives on the caller's stack until `done`, an async one on the heap
+// until its promise is set); results are matched by request, never by position in some shared
+// buffer, so sessions cannot see each other's frames.
 //
 // Reference: SessionManager::send (src/network/SessionManager.cpp:337-388), receive_loop
 // (:703-854) and protocol::encode_signed / decode_signed (src/protocol/Message.cpp:305-328).
@@ -15,6 +19,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <future>
 #include <thread>
 #include <cstring>
 #include <mutex>
@@ -24,8 +29,11 @@
 #include <system_error>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "enet_crypto.h"
 #include "ephemeralnet/crypto/Batch.hpp"
+#include "host_batch.hpp"
 #include "host_engine.hpp"
 #include "scalar.hpp"
 
@@ -42,59 +50,71 @@ struct Req {
     std::vector<std::uint8_t> out;     // frame (send) or message (receive)
     bool ok = false;
     bool done = false;
-    std::condition_variable cv;        // wakes exactly this waiter
+    std::condition_variable cv;        // wakes exactly this waiter (blocking requests)
+    // async requests own their key and input and complete a promise; the flusher deletes them
+    bool async = false;
+    std::array<std::uint8_t, 32> key_own{};
+    std::vector<std::uint8_t> in_own;
+    std::promise<std::optional<std::vector<std::uint8_t>>> prom;
 };
 
-// The batching shared by both directions: one worker thread per queue runs every device pass
-// (started on first use), so the pass's staging buffers and HIP stream are allocated once -- with
-// the lead rotating over the callers, each of 256 session threads paid its own first-use
-// allocations (~1.5 ms per pass at 78 frames).  Callers sleep on their own condition variable and
-// are woken exactly when the pass carrying their frame is done; frames arriving during a pass form
-// the next one (group commit).
+Req* new_async_req(const std::array<std::uint8_t, 32>& key, std::vector<std::uint8_t> in) {
+    auto* r = new Req{};
+    r->async = true;
+    r->key_own = key;
+    r->key = r->key_own.data();
+    r->in_own = std::move(in);
+    r->in = r->in_own;
+    return r;
+}
+
+// The batching shared by both directions: up to max_inflight worker threads per queue (started on
+// first use) run the device passes, each with the pinned staging and HIP stream of its own
+// host-batch engine, so passes overlap one another: while one pass's kernel runs, the next worker
+// gathers the frames that queued up meanwhile.  Blocking callers sleep on their own condition
+// variable and are woken exactly when the pass carrying their frame is done.
 class Flusher {
 public:
-    using Exec = std::function<bool(std::vector<Req*>&)>;  // fills out / ok; true = host engine
+    // fills out / ok of the batch; worker = the calling worker's index; true = host engine served it
+    using Exec = std::function<bool(std::vector<Req*>&, std::size_t worker)>;
     Flusher(const FrameQueueOptions& o, Exec exec) : opt_(o), exec_(std::move(exec)) {
         opt_.max_frames = std::max<std::size_t>(1, opt_.max_frames);
+        opt_.max_inflight = std::min<std::size_t>(std::max<std::size_t>(1, opt_.max_inflight), 16);
     }
     ~Flusher() {
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
         }
-        work_.notify_one();
-        if (worker_.joinable()) worker_.join();
+        work_.notify_all();
+        for (auto& w : workers_)
+            if (w.joinable()) w.join();
     }
 
     void submit(Req& r) {
         std::unique_lock<std::mutex> lk(mu_);
-        if (!worker_.joinable()) {
-            try {
-                worker_ = std::thread([this] { run(); });
-            } catch (const std::system_error&) {  // no thread to be had: serve this frame here
-                lk.unlock();
-                std::vector<Req*> one{&r};
-                bool host = false, failed = false;
-                try {
-                    host = exec_(one);
-                } catch (...) {  // as in run(): the frame fails, nothing escapes to the session
-                    failed = true;
-                    r.ok = false;
-                }
-                lk.lock();
-                r.done = true;
-                if (!failed) {
-                    stats_.frames += 1;
-                    stats_.flushes += 1;
-                    stats_.host_flushes += host ? 1 : 0;
-                }
-                return;
-            }
+        if (!start_workers()) {  // no thread to be had: serve this frame here
+            lk.unlock();
+            serve_inline(r);
+            return;
         }
         pending_.push_back(&r);
         bytes_ += r.in.size();
         work_.notify_one();
         r.cv.wait(lk, [&] { return r.done; });
+    }
+    // the request is owned by the queue from here on (deleted once its promise is set)
+    void submit_async(Req* r) {
+        std::unique_lock<std::mutex> lk(mu_);
+        if (!start_workers()) {
+            lk.unlock();
+            serve_inline(*r);
+            complete(r);
+            return;
+        }
+        pending_.push_back(r);
+        bytes_ += r->in.size();
+        work_.notify_one();
     }
 
     FrameQueueStats stats() {
@@ -110,19 +130,56 @@ public:
     // a mutex here convoyed 256 session threads on 16 cores down to 158 K frames/s)
     void count_direct() { direct_.fetch_add(1, std::memory_order_relaxed); }
 
+    static void complete(Req* r) {  // an async request: fulfil and free it
+        if (r->ok) r->prom.set_value(std::move(r->out));
+        else r->prom.set_value(std::nullopt);
+        delete r;
+    }
+
 private:
     bool full() const { return pending_.size() >= opt_.max_frames || bytes_ >= opt_.max_bytes; }
 
-    void run() {
+    // under mu_: make sure the worker threads run; false when none could be started
+    bool start_workers() {
+        if (!workers_.empty()) return true;
+        try {
+            for (std::size_t w = 0; w < opt_.max_inflight; ++w) workers_.emplace_back([this, w] { run(w); });
+        } catch (const std::system_error&) {
+            if (workers_.empty()) return false;
+        }
+        return true;
+    }
+
+    void serve_inline(Req& r) {
+        std::vector<Req*> one{&r};
+        bool host = false, failed = false;
+        try {
+            host = exec_(one, 0);
+        } catch (...) {  // as in run(): the frame fails, nothing escapes to the session
+            failed = true;
+            r.ok = false;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        r.done = true;
+        if (!failed) {
+            stats_.frames += 1;
+            stats_.flushes += 1;
+            stats_.host_flushes += host ? 1 : 0;
+        }
+    }
+
+    void run(std::size_t w) {
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
             work_.wait(lk, [&] { return stop_ || !pending_.empty(); });
             if (pending_.empty()) return;  // stop_ with nothing queued
-            // no deadline by default (max_delay 0): the batch is whatever queued up during the
-            // previous pass; a positive max_delay also waits for a size limit or the deadline
+            // no deadline by default (max_delay 0): the batch is whatever queued up while the
+            // other workers' passes ran; a positive max_delay also waits for a size limit or the
+            // deadline
             if (opt_.max_delay.count() > 0) {
                 const auto deadline = std::chrono::steady_clock::now() + opt_.max_delay;
                 work_.wait_until(lk, deadline, [&] { return stop_ || full(); });
+                if (pending_.empty()) continue;  // another worker took them
             }
             std::vector<Req*> batch;
             std::size_t take = 0, b = 0;
@@ -134,23 +191,34 @@ private:
             batch.assign(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
             pending_.erase(pending_.begin(), pending_.begin() + (std::ptrdiff_t)take);
             bytes_ -= b;
+            if (!pending_.empty()) work_.notify_one();  // more than one pass queued: wake a peer
             lk.unlock();
             bool host = false, failed = false;
             try {
-                host = exec_(batch);
+                host = exec_(batch, w);
             } catch (...) {  // only std::bad_alloc gets here: fail the batch, keep the queue alive
                 failed = true;
             }
+            std::vector<Req*> async_done;
             lk.lock();
             for (Req* q : batch) {
                 if (failed) q->ok = false;
-                q->done = true;
-                q->cv.notify_one();
+                if (q->async) {
+                    async_done.push_back(q);
+                } else {
+                    q->done = true;
+                    q->cv.notify_one();
+                }
             }
             if (!failed) {
                 stats_.frames += batch.size();
                 stats_.flushes += 1;
                 stats_.host_flushes += host ? 1 : 0;
+            }
+            if (!async_done.empty()) {
+                lk.unlock();
+                for (Req* q : async_done) complete(q);
+                lk.lock();
             }
         }
     }
@@ -164,7 +232,32 @@ private:
     bool stop_ = false;
     FrameQueueStats stats_{};
     std::atomic<std::uint64_t> direct_{0};
-    std::thread worker_;
+    std::vector<std::thread> workers_;
+};
+
+// One host-batch engine per queue worker (single slot: a pass is one chunk), created on first use
+class Engines {
+public:
+    explicit Engines(const FrameQueueOptions& o) : dev_(o.device), e_(std::max<std::size_t>(1, o.max_inflight)) {}
+    ~Engines() {
+        for (auto* e : e_)
+            if (e) enet::hb::destroy_engine(e);
+    }
+    enet::hb::Engine& at(std::size_t w) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto& e = e_[w % e_.size()];
+        if (!e) {
+            enet::hb::Config cfg;
+            cfg.slots = 1;
+            e = enet::hb::create_engine(dev_, cfg);
+        }
+        return *e;
+    }
+
+private:
+    int dev_;
+    std::mutex mu_;
+    std::vector<enet::hb::Engine*> e_;
 };
 
 void put_be32(std::uint8_t* p, std::uint32_t v) {
@@ -284,31 +377,48 @@ void draw_nonces(std::vector<Nonce>& nonces) {
 
 // ------------------------------------------------------------------------------ send
 struct FrameQueue::Impl {
-    explicit Impl(const FrameQueueOptions& o) : flusher(o, [this](std::vector<Req*>& b) { return seal(b); }) {}
+    explicit Impl(const FrameQueueOptions& o)
+        : engines(o), flusher(o, [this](std::vector<Req*>& b, std::size_t w) { return seal(b, &engines.at(w)); }) {}
+    Engines engines;
     Flusher flusher;
     // push / flush
     mutable std::mutex manual_mu;
     std::vector<std::array<std::uint8_t, 32>> keys;
     std::vector<std::vector<std::uint8_t>> messages;
 
-    // seal `batch` (message spans + keys); returns true when the host engine served it
-    bool seal(std::vector<Req*>& batch) {
+    // seal `batch` (message spans + keys) in one device pass through `eng` (the shared engine
+    // when null); returns true when the host engine served it
+    bool seal(std::vector<Req*>& batch, enet::hb::Engine* eng) {
         const std::size_t n = batch.size();
         std::vector<Nonce> nonces(n);
         draw_nonces(nonces);
         if (enet::scalar::g_policy.load() != ENET_SCALAR_HOST) {
-            std::vector<std::array<std::uint8_t, 32>> ks(n);
+            std::vector<std::uint8_t> ks(32 * n);
             std::vector<std::span<const std::uint8_t>> ms(n);
+            std::vector<std::vector<std::uint8_t>*> outs(n);
             for (std::size_t i = 0; i < n; ++i) {
-                std::memcpy(ks[i].data(), batch[i]->key, 32);
+                std::memcpy(ks.data() + 32 * i, batch[i]->key, 32);
                 ms[i] = batch[i]->in;
+                outs[i] = &batch[i]->out;
             }
-            std::vector<std::vector<std::uint8_t>> frames;
-            if (enet::scalar::try_device("FrameQueue flush", [&] { frames = wire_seal(ks, nonces, ms); })) {
-                for (std::size_t i = 0; i < n; ++i) {
-                    batch[i]->out = std::move(frames[i]);
-                    batch[i]->ok = true;
+            const bool dev_ok = enet::scalar::try_device("FrameQueue flush", [&] {
+                enet::hb::Job j;
+                j.op = enet::hb::Op::WireSeal;
+                j.n = n;
+                j.in_spans = ms;
+                j.out_each = outs;
+                j.keys = ks.data();
+                j.nonces = reinterpret_cast<const std::uint8_t*>(nonces.data());
+                if (eng) {
+                    enet::hb::run(*eng, j);
+                } else {
+                    int dev = 0;
+                    (void)hipGetDevice(&dev);
+                    enet::hb::run(enet::hb::shared_engine(dev), j);
                 }
+            });
+            if (dev_ok) {
+                for (std::size_t i = 0; i < n; ++i) batch[i]->ok = true;
                 return false;
             }
         }
@@ -345,6 +455,19 @@ std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::
     return std::move(r.out);
 }
 
+std::future<std::optional<std::vector<std::uint8_t>>> FrameQueue::seal_async(
+    const std::array<std::uint8_t, 32>& session_key, std::vector<std::uint8_t> message) {
+    if (message.size() + kMac > kMaxPayloadSize || enet::scalar::g_policy.load() != ENET_SCALAR_DEVICE) {
+        std::promise<std::optional<std::vector<std::uint8_t>>> p;
+        p.set_value(seal(session_key, message));  // refused, or the host engine on this thread
+        return p.get_future();
+    }
+    Req* r = new_async_req(session_key, std::move(message));
+    auto f = r->prom.get_future();
+    impl_->flusher.submit_async(r);
+    return f;
+}
+
 bool FrameQueue::push(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message) {
     if (message.size() + kMac > kMaxPayloadSize) return false;
     std::lock_guard<std::mutex> lk(impl_->manual_mu);
@@ -374,7 +497,7 @@ std::vector<std::vector<std::uint8_t>> FrameQueue::flush() {
         batch[i] = &reqs[i];
     }
     std::vector<std::vector<std::uint8_t>> frames(messages.size());
-    if (!batch.empty()) impl_->seal(batch);
+    if (!batch.empty()) impl_->seal(batch, nullptr);
     for (std::size_t i = 0; i < frames.size(); ++i) frames[i] = std::move(reqs[i].out);
     return frames;
 }
@@ -383,24 +506,36 @@ FrameQueueStats FrameQueue::stats() const { return impl_->flusher.stats(); }
 
 // ------------------------------------------------------------------------------ receive
 struct FrameReceiveQueue::Impl {
-    explicit Impl(const FrameQueueOptions& o) : flusher(o, [this](std::vector<Req*>& b) { return open(b); }) {}
+    explicit Impl(const FrameQueueOptions& o)
+        : engines(o), flusher(o, [this](std::vector<Req*>& b, std::size_t w) { return open(b, engines.at(w)); }) {}
+    Engines engines;
     Flusher flusher;
 
-    bool open(std::vector<Req*>& batch) {
+    bool open(std::vector<Req*>& batch, enet::hb::Engine& eng) {
         const std::size_t n = batch.size();
         if (enet::scalar::g_policy.load() != ENET_SCALAR_HOST) {
-            std::vector<std::array<std::uint8_t, 32>> ks(n);
+            std::vector<std::uint8_t> ks(32 * n), ok(n, 0);
             std::vector<std::span<const std::uint8_t>> fs(n);
+            std::vector<std::vector<std::uint8_t>*> outs(n);
             for (std::size_t i = 0; i < n; ++i) {
-                std::memcpy(ks[i].data(), batch[i]->key, 32);
+                std::memcpy(ks.data() + 32 * i, batch[i]->key, 32);
                 fs[i] = batch[i]->in;
+                outs[i] = &batch[i]->out;
             }
-            std::vector<std::vector<std::uint8_t>> msgs;
-            std::vector<std::uint8_t> ok;
-            if (enet::scalar::try_device("FrameReceiveQueue flush", [&] { msgs = wire_open(ks, fs, ok); })) {
+            const bool dev_ok = enet::scalar::try_device("FrameReceiveQueue flush", [&] {
+                enet::hb::Job j;
+                j.op = enet::hb::Op::WireOpen;
+                j.n = n;
+                j.in_spans = fs;
+                j.out_each = outs;
+                j.keys = ks.data();
+                j.ok_out = ok.data();
+                enet::hb::run(eng, j);
+            });
+            if (dev_ok) {
                 for (std::size_t i = 0; i < n; ++i) {
                     batch[i]->ok = ok[i] == 1;
-                    if (batch[i]->ok) batch[i]->out = std::move(msgs[i]);
+                    if (!batch[i]->ok) batch[i]->out.clear();
                 }
                 return false;
             }
@@ -429,6 +564,19 @@ std::optional<std::vector<std::uint8_t>> FrameReceiveQueue::open(const std::arra
     impl_->flusher.submit(r);
     if (!r.ok) return std::nullopt;
     return std::move(r.out);
+}
+
+std::future<std::optional<std::vector<std::uint8_t>>> FrameReceiveQueue::open_async(
+    const std::array<std::uint8_t, 32>& session_key, std::vector<std::uint8_t> frame) {
+    if (!frame_shape_ok(frame) || enet::scalar::g_policy.load() != ENET_SCALAR_DEVICE) {
+        std::promise<std::optional<std::vector<std::uint8_t>>> p;
+        p.set_value(open(session_key, frame));  // bad shape, or the host engine on this thread
+        return p.get_future();
+    }
+    Req* r = new_async_req(session_key, std::move(frame));
+    auto f = r->prom.get_future();
+    impl_->flusher.submit_async(r);
+    return f;
 }
 
 FrameQueueStats FrameReceiveQueue::stats() const { return impl_->flusher.stats(); }

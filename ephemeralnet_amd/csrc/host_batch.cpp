@@ -241,6 +241,8 @@ Layout layout(const Job& j, uint32_t m) {
 
 std::atomic<int> g_mode{-1};
 
+std::vector<uint8_t>& vec_of(const Job& j, size_t i) { return j.out_vecs ? (*j.out_vecs)[i] : *j.out_each[i]; }
+
 }  // namespace
 
 int64_t out_delta(Op op) { return delta_of(op); }
@@ -508,8 +510,8 @@ void Engine::finish(Slot& s, const Job& j) {
         std::memcpy(j.macs_out + 32ull * c0, sm + l.macs_out, 32ull * m);
     if (j.ok_out && is_open(j.op)) std::memcpy(j.ok_out + c0, sm + l.ok, m);
     if (s.direct_out || s.out_b == 0) {
-        if (j.out_vecs)
-            for (size_t i = c0; i < c1; ++i) (*j.out_vecs)[i].clear();
+        if (j.out_vecs || !j.out_each.empty())
+            for (size_t i = c0; i < c1; ++i) vec_of(j, i).clear();
         return;
     }
     const uint8_t* base = s.out.h;
@@ -524,8 +526,8 @@ void Engine::finish(Slot& s, const Job& j) {
         uint64_t r = at[p];
         for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
             const uint64_t len = lout_[i];
-            if (j.out_vecs) {
-                auto& v = (*j.out_vecs)[i];
+            if (j.out_vecs || !j.out_each.empty()) {
+                auto& v = vec_of(j, i);
                 v.resize(len);
                 if (len) std::memcpy(v.data(), base + r, len);
             } else if (len) {
@@ -543,7 +545,9 @@ void Engine::run(const Job& j) {
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("enet host batch: more than 2^32 - 1 records");
     if (!j.in_spans.empty() ? j.in_spans.size() != n : (!j.in_base || !j.in_off))
         throw std::invalid_argument("enet host batch: input records missing");
-    if (!j.out_vecs && (!j.out_base || !j.out_off)) throw std::invalid_argument("enet host batch: output missing");
+    const bool vec_out = j.out_vecs || !j.out_each.empty();
+    if (!j.out_each.empty() && j.out_each.size() != n) throw std::invalid_argument("enet host batch: out_each size");
+    if (!vec_out && (!j.out_base || !j.out_off)) throw std::invalid_argument("enet host batch: output missing");
     if (!j.keys) throw std::invalid_argument("enet host batch: keys missing");
     if (j.key_stride != 0 && j.key_stride != 32) throw std::invalid_argument("enet host batch: key_stride must be 0 or 32");
     if (!j.nonces && j.op != Op::WireOpen) throw std::invalid_argument("enet host batch: nonces missing");
@@ -575,13 +579,13 @@ void Engine::run(const Job& j) {
         lout_[i] = (uint64_t)std::max<int64_t>(0, (int64_t)a + delta);
         in_total += a;
         out_total += lout_[i];
-        if (!j.out_vecs && j.out_off[i + 1] - j.out_off[i] != lout_[i])
+        if (!vec_out && j.out_off[i + 1] - j.out_off[i] != lout_[i])
             throw std::invalid_argument("enet host batch: output offsets do not give the op's output lengths");
     }
     if (j.out_vecs) j.out_vecs->resize(n);
     // in place where the caller's arenas are device-accessible
     in_dev_ = j.in_spans.empty() ? device_view(j.in_base + j.in_off[0], in_total) : nullptr;
-    out_dev_ = j.out_vecs ? nullptr : device_view(j.out_base + j.out_off[0], out_total);
+    out_dev_ = vec_out ? nullptr : device_view(j.out_base + j.out_off[0], out_total);
     if (in_dev_) in_dev_ -= j.in_off[0];
     if (out_dev_) out_dev_ -= j.out_off[0];
     const bool direct_out = out_dev_ != nullptr;

@@ -49,6 +49,8 @@ struct Job {
     // output record i (|out_i| = max(0, |in_i| + out_delta(op))): out_vecs[i] (resized here) when
     // set, else out_base[out_off[i] .. out_off[i+1]) (the caller's offsets must give that length)
     std::vector<std::vector<uint8_t>>* out_vecs = nullptr;
+    // ... or out_each[i] (one caller-owned vector per record, e.g. queued requests; resized here)
+    std::span<std::vector<uint8_t>* const> out_each;
     uint8_t* out_base = nullptr;
     const uint64_t* out_off = nullptr;
     // per-record small inputs (host memory)

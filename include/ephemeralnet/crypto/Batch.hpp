@@ -7,6 +7,7 @@
 #include <array>
 #include <chrono>
 #include <cstdint>
+#include <future>
 #include <optional>
 #include <span>
 #include <string_view>
@@ -137,6 +138,9 @@ struct FrameQueueOptions {
     std::size_t max_bytes = 8u << 20;                  // ... and this many bytes
     std::chrono::microseconds max_delay{0};            // > 0: before a pass, wait this long (or
                                                        // for a size limit) for more frames
+    std::size_t max_inflight = 4;                      // device passes in flight at once (one
+                                                       // worker thread + pinned staging each)
+    int device = 0;                                    // HIP device of the device passes
 };
 struct FrameQueueStats {
     std::uint64_t frames = 0;   // frames served
@@ -162,6 +166,13 @@ public:
     // SessionManager::send returns false (:358-360).
     std::optional<std::vector<std::uint8_t>> seal(const std::array<std::uint8_t, 32>& session_key,
                                                   std::span<const std::uint8_t> message);
+    // Non-blocking seal: the queue takes the message, the future becomes ready when the pass
+    // carrying it has run (nullopt as seal()).  One thread can keep thousands of frames in flight,
+    // so passes grow with the offered load instead of with the number of blocked threads.  Under
+    // the auto / host policies the frame is sealed on the calling thread and the future is ready
+    // on return.
+    std::future<std::optional<std::vector<std::uint8_t>>> seal_async(const std::array<std::uint8_t, 32>& session_key,
+                                                                      std::vector<std::uint8_t> message);
     // Explicit batching (a sender that collects frames itself): push queues a message (false =
     // too large, nothing queued), flush() seals every pushed message in one pass and returns the
     // wire frames in push order.  Thread-safe; independent of seal()'s queue.
@@ -189,6 +200,9 @@ public:
 
     std::optional<std::vector<std::uint8_t>> open(const std::array<std::uint8_t, 32>& session_key,
                                                   std::span<const std::uint8_t> frame);
+    // Non-blocking open (see FrameQueue::seal_async).
+    std::future<std::optional<std::vector<std::uint8_t>>> open_async(const std::array<std::uint8_t, 32>& session_key,
+                                                                     std::vector<std::uint8_t> frame);
     FrameQueueStats stats() const;
 
 private:

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <future>
 #include <string>
 #include <thread>
 #include <vector>
@@ -73,7 +74,62 @@ int nonce_uniqueness(const std::string& policy, int T, int F) {
     return distinct == (std::ptrdiff_t)all.size() ? 0 : 1;
 }
 
+// async <policy> <threads> <frames>: every thread submits ALL its frames with seal_async before
+// waiting for any (then the same with open_async, every 5th frame tampered), so a device pass can
+// carry frames of many threads and many frames of one thread.  Prints a summary line.
+int async_mode(const std::string& policy, int T, int F) {
+    enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
+                                                                                      : ENET_SCALAR_AUTO, 0);
+    FrameQueue tx;
+    FrameReceiveQueue rx;
+    std::atomic<int> bad{0}, opened{0}, rejected{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            std::uint64_t s = 77 + (std::uint64_t)t;
+            std::array<std::uint8_t, 32> key{};
+            for (auto& b : key) b = (std::uint8_t)splitmix(s);
+            std::vector<std::vector<std::uint8_t>> msgs(F);
+            for (auto& m : msgs) {
+                m.resize(splitmix(s) % 2049);
+                for (auto& b : m) b = (std::uint8_t)splitmix(s);
+            }
+            std::vector<std::future<std::optional<std::vector<std::uint8_t>>>> fs;
+            for (auto& m : msgs) fs.push_back(tx.seal_async(key, m));
+            std::vector<std::vector<std::uint8_t>> frames(F);
+            for (int i = 0; i < F; ++i) {
+                auto f = fs[i].get();
+                if (!f || f->size() != msgs[i].size() + 48) { ++bad; continue; }
+                frames[i] = std::move(*f);
+            }
+            fs.clear();
+            for (int i = 0; i < F; ++i) {
+                auto f = frames[i];
+                if (i % 5 == 2 && f.size() > 20) f[20] ^= 0x08;  // body byte
+                fs.push_back(rx.open_async(key, std::move(f)));
+            }
+            for (int i = 0; i < F; ++i) {
+                auto m = fs[i].get();
+                const bool expect = !(i % 5 == 2 && frames[i].size() > 20);
+                if (m) ++opened;
+                else ++rejected;
+                if ((bool)m != expect || (m && *m != msgs[i])) ++bad;
+            }
+        });
+    for (auto& x : th) x.join();
+    const auto st = tx.stats(), sr = rx.stats();
+    std::printf("summary bad=%d opened=%d rejected=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu "
+                "rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu\n",
+                bad.load(), opened.load(), rejected.load(), (unsigned long long)st.frames,
+                (unsigned long long)st.flushes, (unsigned long long)st.host_flushes, (unsigned long long)sr.frames,
+                (unsigned long long)sr.flushes, (unsigned long long)sr.host_flushes);
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "async")
+        return async_mode(argc > 2 ? argv[2] : "device", argc > 3 ? std::atoi(argv[3]) : 8,
+                          argc > 4 ? std::atoi(argv[4]) : 500);
     if (argc > 1 && std::string(argv[1]) == "nonces")
         return nonce_uniqueness(argc > 2 ? argv[2] : "auto", argc > 3 ? std::atoi(argv[3]) : 8,
                                 argc > 4 ? std::atoi(argv[4]) : 10000);

@@ -1,0 +1,103 @@
+// queue_bench.cpp -- session-frame throughput of the cross-session queues (Batch.hpp FrameQueue /
+// FrameReceiveQueue) for MTU frames, blocking and asynchronous submission.
+//
+//   sync  : T session threads, each seal()s (then open()s) one frame at a time, as
+//           SessionManager::send / receive_loop do (SessionManager.cpp:337-388, 703-854)
+//   async : T threads, each keeps W frames in flight with seal_async() / open_async() (a relay
+//           draining a socket buffer), so a device pass can carry T x W frames
+// for the policies device / auto / host (enet_scalar_set_policy).  JSON line per case: frames/s
+// each direction, frames per pass, passes served by the host engine.
+//
+// build: hipcc --offload-arch=gfx950 -O2 -std=c++20 -Iinclude tools/queue_bench.cpp
+//        -Lephemeralnet_amd -lenet_crypto -Wl,-rpath,'$ORIGIN/../ephemeralnet_amd' -o tools/queue_bench
+// usage: queue_bench <policy> <sync|async> <threads> [window] [seconds] [bytes] [inflight]
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "enet_crypto.h"
+#include "ephemeralnet/crypto/Batch.hpp"
+
+using namespace ephemeralnet::crypto;
+using Clock = std::chrono::steady_clock;
+
+int main(int argc, char** argv) {
+    const std::string pol = argc > 1 ? argv[1] : "device";
+    const std::string mode = argc > 2 ? argv[2] : "sync";
+    const int T = argc > 3 ? std::atoi(argv[3]) : 16;
+    const int W = argc > 4 ? std::atoi(argv[4]) : 64;
+    const double secs = argc > 5 ? std::atof(argv[5]) : 1.5;
+    const size_t L = argc > 6 ? (size_t)std::atoll(argv[6]) : 1500;
+    const size_t inflight = argc > 7 ? (size_t)std::atoll(argv[7]) : 4;
+    enet_scalar_set_policy(pol == "device" ? ENET_SCALAR_DEVICE : pol == "host" ? ENET_SCALAR_HOST : ENET_SCALAR_AUTO, 0);
+    batch::FrameQueueOptions opt;
+    opt.max_inflight = inflight;
+    batch::FrameQueue tx(opt);
+    batch::FrameReceiveQueue rx(opt);
+    std::vector<std::array<uint8_t, 32>> keys(T);
+    for (int t = 0; t < T; ++t)
+        for (int i = 0; i < 32; ++i) keys[t][i] = (uint8_t)(i * 7 + t);
+    std::vector<uint8_t> msg(L);
+    for (size_t i = 0; i < L; ++i) msg[i] = (uint8_t)(i * 13);
+    std::vector<std::vector<uint8_t>> wire(T);
+    for (int t = 0; t < T; ++t) wire[t] = *tx.seal(keys[t], msg);  // warm-up and the frames to open
+    std::atomic<bool> bad{false};
+
+    auto run = [&](bool seal_side) {
+        std::atomic<bool> stop{false};
+        std::atomic<uint64_t> done{0};
+        std::vector<std::thread> th;
+        const auto t0 = Clock::now();
+        for (int t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                uint64_t n = 0;
+                if (mode == "sync") {
+                    while (!stop.load(std::memory_order_relaxed)) {
+                        auto r = seal_side ? tx.seal(keys[t], msg) : rx.open(keys[t], wire[t]);
+                        if (!r || r->size() != (seal_side ? L + 48 : L)) bad = true;
+                        ++n;
+                    }
+                } else {
+                    std::deque<std::future<std::optional<std::vector<uint8_t>>>> q;
+                    while (!stop.load(std::memory_order_relaxed)) {
+                        while ((int)q.size() < W)
+                            q.push_back(seal_side ? tx.seal_async(keys[t], msg) : rx.open_async(keys[t], wire[t]));
+                        auto r = q.front().get();
+                        q.pop_front();
+                        if (!r || r->size() != (seal_side ? L + 48 : L)) bad = true;
+                        ++n;
+                    }
+                    for (auto& f : q) (void)f.get();
+                }
+                done += n;
+            });
+        std::this_thread::sleep_for(std::chrono::duration<double>(secs));
+        stop = true;
+        for (auto& x : th) x.join();
+        const double el = std::chrono::duration<double>(Clock::now() - t0).count();
+        return done.load() / el;
+    };
+    const auto s0 = tx.stats(), r0 = rx.stats();
+    const double seal_fps = run(true);
+    const double open_fps = run(false);
+    const auto s1 = tx.stats(), r1 = rx.stats();
+    const double tx_pass = (double)(s1.frames - s0.frames) / std::max<uint64_t>(1, s1.flushes - s0.flushes);
+    const double rx_pass = (double)(r1.frames - r0.frames) / std::max<uint64_t>(1, r1.flushes - r0.flushes);
+    enet_scalar_stats st{};
+    enet_scalar_get_stats(&st);
+    std::printf("{\"policy\":\"%s\",\"mode\":\"%s\",\"threads\":%d,\"window\":%d,\"bytes\":%zu,\"inflight\":%zu,"
+                "\"seal_frames_per_s\":%.0f,\"open_frames_per_s\":%.0f,\"tx_frames_per_pass\":%.1f,"
+                "\"rx_frames_per_pass\":%.1f,\"tx_host_passes\":%llu,\"rx_host_passes\":%llu,"
+                "\"device_failures\":%llu,\"ok\":%d}\n",
+                pol.c_str(), mode.c_str(), T, mode == "sync" ? 1 : W, L, inflight, seal_fps, open_fps, tx_pass,
+                rx_pass, (unsigned long long)(s1.host_flushes - s0.host_flushes),
+                (unsigned long long)(r1.host_flushes - r0.host_flushes), (unsigned long long)st.device_failures,
+                bad ? 0 : 1);
+    return bad ? 1 : 0;
+}
