@@ -66,12 +66,14 @@ def parse():
                     help="host-resident path through the library's host pipeline: pinned host "
                          "buffers, H2D -> kernel -> D2H overlapped over --streams streams in "
                          "--chunk-mib chunks (recorded in DESIGN.md, never `value`)")
-    ap.add_argument("--chunk-mib", type=int, default=16, help="host pipeline chunk size")
-    ap.add_argument("--streams", type=int, default=3, help="host pipeline streams")
-    ap.add_argument("--c5-chunk-mib", type=int, default=256,
+    ap.add_argument("--chunk-mib", type=int, default=0, help="host pipeline chunk size (0 = runtime default)")
+    ap.add_argument("--streams", type=int, default=0, help="host pipeline slots / streams (0 = runtime default)")
+    ap.add_argument("--no-host", action="store_true",
+                    help="default line: skip the host-resident extra keys (C2 e2e, C5 per-GPU share)")
+    ap.add_argument("--c5-chunk-mib", type=int, default=0,
                     help="host pipeline chunk size for --c5 (one lane hashes a whole record, so "
                          "mixed batches with HMAC want big chunks)")
-    ap.add_argument("--c5-streams", type=int, default=6,
+    ap.add_argument("--c5-streams", type=int, default=0,
                     help="host pipeline streams for --c5 (a chunk's kernel lasts as long as its "
                          "longest record's serial HMAC, so more chunks in flight)")
     ap.add_argument("--c5", action="store_true",
@@ -265,16 +267,15 @@ def cpu_reference_frames(record_bytes: int, budget_s: float) -> dict | None:
                       f"ChaCha20, oracle/_ref compiled from src/crypto), {threads} threads"}
 
 
-def e2e(args) -> dict:
-    """Seal and open with the data starting and ending in pinned host memory, as the reference's
-    socket/relay path does, through the library's host pipeline (enet_pipeline_aead_*: chunks
-    of --chunk-mib on --streams HIP streams, H2D -> kernel -> D2H overlapped).  Keys, nonces and
-    tags live on the host too and travel with their chunk."""
+def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, streams: int = 0) -> dict:
+    """C2 shape starting and ending in pinned host memory (the reference's socket / relay path),
+    through the library's host pipeline (enet_pipeline_aead_*, host_batch.cpp runtime): seal then
+    open, `reps` each, every tag verified and the plaintext back byte for byte.  Keys, nonces and
+    tags live on the host too.  Returns GiB/s of plaintext (sum L / (t_seal + t_open))."""
     import torch
 
     import ephemeralnet_amd as E
 
-    n, L = args.records, args.record_bytes
     g = torch.Generator().manual_seed(7)
     pt_h = torch.randint(0, 256, (n * L,), dtype=torch.uint8, generator=g).pin_memory()
     keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
@@ -286,10 +287,9 @@ def e2e(args) -> dict:
     ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
-    pipe = E.Pipeline(0, args.chunk_mib << 20, args.streams)
+    pipe = E.Pipeline(dev_index, chunk_mib << 20, streams)
     pipe.aead_seal(seal_b, ct_h, tags_h)  # warm-up (grows the pipeline's buffers)
     pipe.aead_open(open_b, back_h, tags_h, ok_h)
-    reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
         pipe.aead_seal(seal_b, ct_h, tags_h)
@@ -298,17 +298,25 @@ def e2e(args) -> dict:
         pipe.aead_open(open_b, back_h, tags_h, ok_h)
     t2 = time.perf_counter()
     pipe.close()
-    assert int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
+    if int(ok_h.sum()) != n or not torch.equal(back_h, pt_h):
+        raise SystemExit("host-resident C2: round trip failed")
     gib = n * L * reps / 2**30
+    return {"gibs": gib / (t2 - t0), "seal_gibs": gib / (t1 - t0), "open_gibs": gib / (t2 - t1)}
+
+
+def e2e(args) -> dict:
+    """--e2e: the C2 shape host-resident (host_c2), one line."""
+    import ephemeralnet_amd as E
+    r = host_c2(0, args.records, args.record_bytes, 3, args.chunk_mib, args.streams)
     return {
         "metric": "GiB/s ChaCha20-Poly1305 seal+open, host-resident (H2D + kernel + D2H)",
-        "value": round(gib / (t2 - t0), 2),
+        "value": round(r["gibs"], 2),
         "unit": "GiB/s",
-        "seal_GiBs": round(gib / (t1 - t0), 2),
-        "open_GiBs": round(gib / (t2 - t1), 2),
+        "seal_GiBs": round(r["seal_gibs"], 2),
+        "open_GiBs": round(r["open_gibs"], 2),
         "pcie_bytes_per_plaintext_byte": 2.0,
-        "config": {"records": n, "record_bytes": L, "chunk_mib": args.chunk_mib,
-                   "streams": args.streams, "host_buffers": "pinned",
+        "config": {"records": args.records, "record_bytes": args.record_bytes, "chunk_mib": args.chunk_mib,
+                   "streams": args.streams, "host_buffers": "pinned", "host_mode": E.host_mode(),
                    "path": "enet_pipeline_aead_seal/open (libenet_crypto.so)"},
     }
 
@@ -404,34 +412,26 @@ def dist_init(local: int):
     return dev, torch.device("cpu")
 
 
-def c5(args) -> dict:
-    """SURVEY 8d C5: mixed log-uniform 512 B-64 KiB records with the fused HMAC-SHA256 tag,
-    starting and ending in pinned host memory, through the library's host pipeline
-    (enet_pipeline_aead_hmac_*).  Multi-GPU: each rank takes a byte-balanced contiguous share
-    (shard.py), no collective."""
+def c5_lengths(n_all: int):
+    """SURVEY 8d C5 record lengths: log-uniform on [512, 65 536] B, seed 5."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    return np.exp(rng.uniform(np.log(512), np.log(65536), n_all)).astype(np.int64)
+
+
+def host_c5_rank(dev_index: int, lens, seed: int, chunk_mib: int, streams: int, steps: int = 1):
+    """One rank's share of C5 host-resident: AEAD + fused HMAC-SHA256 seal then open of `lens`
+    records from and to pinned host memory (enet_pipeline_aead_hmac_*).  Returns (step(),
+    check(), bytes): step() runs one seal+open, check() verifies the last round trip."""
     import numpy as np
     import torch
-    import torch.distributed as dist
 
     import ephemeralnet_amd as E
-    from ephemeralnet_amd.shard import shard_ranges
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = red_dev = torch.device("cuda", local)
-    if world > 1:
-        dev, red_dev = dist_init(local)
-    rng = np.random.default_rng(5)
-    # BASELINE config 5: n = 524 288 records (~7 GB) unless --records says otherwise
-    n_all = (args.records if args.records_given else 524288) * world
-    lens_all = np.exp(rng.uniform(np.log(512), np.log(65536), n_all)).astype(np.int64)
-    lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
-    lens = lens_all[lo:hi]
     n = len(lens)
     offs_h = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).pin_memory()
     total = int(offs_h[-1])
-    g = torch.Generator().manual_seed(11 + rank)
+    g = torch.Generator().manual_seed(seed)
     pt_h = torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g).pin_memory()
     keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
     nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
@@ -443,37 +443,84 @@ def c5(args) -> dict:
     mx = int(lens.max()) if n else 0
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
-    pipe = E.Pipeline(dev.index, args.c5_chunk_mib << 20, args.c5_streams)
+    pipe = E.Pipeline(dev_index, chunk_mib << 20, streams)
 
     def step():
         pipe.aead_hmac_seal(seal_b, ct_h, tags_h, macs_h)
         pipe.aead_hmac_open(open_b, back_h, tags_h, macs_h, ok_h)
 
-    step()
+    def check():
+        good = int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
+        pipe.close()
+        return good
+
+    return step, check, total
+
+
+def c5_host_timed(world: int, rank: int, dev_index: int, red_dev, n_per_rank: int, chunk_mib: int,
+                  streams: int, steps: int = 1) -> dict:
+    """C5 host-resident over all ranks: the n_per_rank * world records are split into byte-balanced
+    contiguous shares (shard.py, no collective on the data path); every rank seals and opens its
+    share, barrier + max-over-ranks time; GiB/s = all ranks' plaintext bytes / that time."""
+    import torch
+    import torch.distributed as dist
+
+    from ephemeralnet_amd.shard import shard_ranges
+
+    lens_all = c5_lengths(n_per_rank * world)
+    lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
+    step, check, mine = host_c5_rank(dev_index, lens_all[lo:hi], 11 + rank, chunk_mib, streams)
+    step()  # warm-up: grows the pipeline's staging
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    step()
+    for _ in range(steps):
+        step()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    ok = check()
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    pipe.close()
-    assert int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
+        el, bad = float(t[0].item()), float(t[1].item())
+        ok = bad == 0.0
+    if not ok:
+        raise SystemExit(f"rank {rank}: C5 host-resident round trip failed")
+    return {"gibs": int(lens_all.sum()) * steps / el / 2**30, "records_total": len(lens_all),
+            "bytes_total": int(lens_all.sum()), "seconds": el}
+
+
+def c5(args) -> dict:
+    """SURVEY 8d C5: mixed log-uniform 512 B-64 KiB records with the fused HMAC-SHA256 tag,
+    starting and ending in pinned host memory, through the library's host pipeline
+    (enet_pipeline_aead_hmac_*).  Multi-GPU: each rank takes a byte-balanced contiguous share
+    (shard.py), no collective."""
+    import torch
+    import torch.distributed as dist
+
+    import ephemeralnet_amd as E
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = red_dev = torch.device("cuda", local)
+    if world > 1:
+        dev, red_dev = dist_init(local)
+    # BASELINE config 5: n = 524 288 records (~7 GB) unless --records says otherwise
+    n_per = args.records if args.records_given else 524288
+    r = c5_host_timed(world, rank, dev.index, red_dev, n_per, args.c5_chunk_mib, args.c5_streams)
     res = None
     if rank == 0:
         res = {
             "metric": "GiB/s AEAD + fused HMAC-SHA256 seal+open, mixed 512 B-64 KiB, "
                       "host-resident (H2D + kernels + D2H)",
-            "value": round(int(lens_all.sum()) / el / 2**30, 2),
+            "value": round(r["gibs"], 2),
             "unit": "GiB/s",
             "n_gpus": world,
-            "config": {"workload": "C5", "records_total": n_all, "bytes_total": int(lens_all.sum()),
+            "config": {"workload": "C5", "records_total": r["records_total"], "bytes_total": r["bytes_total"],
                        "chunk_mib": args.c5_chunk_mib, "streams": args.c5_streams,
-                       "host_buffers": "pinned",
+                       "host_buffers": "pinned", "host_mode": E.host_mode(),
                        "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
     if world > 1:
@@ -870,6 +917,25 @@ def main():
     if sampler is not None:
         power = sample_power(sampler, lambda: (seal(), open_()), lambda: torch.cuda.synchronize(dev))
 
+    # Host-resident extra keys (never `value`): the reference's path starts and ends in host
+    # memory (SessionManager.cpp:1049-1099), so the line also carries the C2 shape through the
+    # host pipeline and BASELINE config 5 (mixed 512 B-64 KiB, AEAD + fused HMAC, H2D/D2H
+    # included) at its per-GPU share, 524 288 / 8 = 65 536 records per rank, timed over all ranks
+    host = None
+    if args.mode == "aead" and not args.no_host and (n, L) == (65536, 4096):
+        import ephemeralnet_amd as E2
+        hc2 = host_c2(dev.index, n, L, 3, args.chunk_mib, args.streams)
+        hc5 = c5_host_timed(world, rank, dev.index, red_dev, 65536, args.c5_chunk_mib, args.c5_streams)
+        host = {"e2e_gibs": round(hc2["gibs"], 2), "e2e_seal_gibs": round(hc2["seal_gibs"], 2),
+                "e2e_open_gibs": round(hc2["open_gibs"], 2),
+                "e2e_is": "C2 (65 536 x 4 KiB) seal+open from and to pinned host memory, this rank",
+                "c5_host_gibs": round(hc5["gibs"], 2),
+                "c5_host_is": f"BASELINE config 5 per-GPU share: {hc5['records_total']} log-uniform "
+                              f"512 B-64 KiB records over {world} rank(s), AEAD + fused HMAC-SHA256 "
+                              "seal+open, pinned host memory in and out, all ranks' bytes / max-over-ranks time",
+                "host_mode": "zero-copy" if E2.host_mode() == 0 else "sdma",
+                "path": "enet_pipeline_aead_* / enet_pipeline_aead_hmac_* (host_batch.cpp)"}
+
     if rank == 0:
         total_bytes = n * L * args.steps * world
         value = total_bytes / elapsed / 2**30
@@ -980,6 +1046,8 @@ def main():
         }
         if power:
             out["power"] = power
+        if host:
+            out["host_resident"] = host
         if ranks is not None:
             out["dist"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
                            "per_rank": ranks}

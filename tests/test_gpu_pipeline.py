@@ -21,6 +21,16 @@ def enet():
     yield E
 
 
+@pytest.fixture(params=[0, 1], ids=["zerocopy", "sdma"])
+def mode(enet, request):
+    """Both ways the host runtime reaches host memory (enet_host_set_mode): zero-copy kernels on
+    pinned staging, and SDMA copies into device arenas.  Same bytes either way."""
+    prev = enet.host_mode()
+    enet.set_host_mode(request.param)
+    yield request.param
+    enet.set_host_mode(prev)
+
+
 def host_batch(E, items, keys, nonces, pinned, key_stride=32):
     import torch
     offs = np.concatenate([[0], np.cumsum([len(x) for x in items])]).astype(np.int64)
@@ -51,7 +61,7 @@ def records(t, offs):
                                                           (True, False, 4, 100000),
                                                           (False, False, 2, 70000),
                                                           (True, True, 1, 1 << 30)])
-def test_pipeline_aead_roundtrip_vs_oracle(enet, pinned, uniform, streams, chunk):
+def test_pipeline_aead_roundtrip_vs_oracle(enet, mode, pinned, uniform, streams, chunk):
     import torch
     n = 257
     if uniform:
@@ -91,7 +101,7 @@ def test_pipeline_aead_roundtrip_vs_oracle(enet, pinned, uniform, streams, chunk
                 assert okh[i] == 1 and bk[i] == items[i], i
 
 
-def test_pipeline_hmac_and_xor_vs_oracle(enet):
+def test_pipeline_hmac_and_xor_vs_oracle(enet, mode):
     import torch
     n = 90
     raw = np.frombuffer(splitmix_bytes(77, 4 * n), dtype="<u4")
@@ -193,3 +203,85 @@ def test_pipeline_group_vs_single(enet, devices):
         assert mh[32 * i:32 * i + 32] == oracle.hmac_sha256(keys[i], items[i]), i
     for i in range(n):
         assert (okh[i], back[i]) == ((0, bytes(lens[i])) if i in (3, n - 2) else (1, items[i])), i
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_pipeline_wire_frames_vs_oracle(enet, mode, pinned):
+    """enet_pipeline_wire_seal / wire_open: whole wire frames nonce || BE32 || ChaCha20(m || HMAC)
+    from and to host memory (SessionManager.cpp:362-387, 760-822), ragged lengths 0..3000 and one
+    64 KiB message, small chunks so the batch spans many; a tampered frame is rejected and zeroed."""
+    import torch
+    n = 300
+    raw = np.frombuffer(splitmix_bytes(31, 4 * n), dtype="<u4")
+    lens = [int(x % 3001) for x in raw]
+    lens[5], lens[6] = 0, 65536
+    msgs = [splitmix_bytes(11000 + i, L) for i, L in enumerate(lens)]
+    keys = [splitmix_bytes(12000 + i, 32) for i in range(n)]
+    nonces = [splitmix_bytes(13000 + i, 12) for i in range(n)]
+    b = host_batch(enet, msgs, keys, nonces, pinned)
+    foffs = torch.from_numpy(np.concatenate([[0], np.cumsum([L + 48 for L in lens])]).astype(np.int64))
+    frames = torch.zeros(int(foffs[-1]), dtype=torch.uint8)
+    if pinned:
+        foffs, frames = foffs.pin_memory(), frames.pin_memory()
+    with enet.Pipeline(0, 120000, 3) as pipe:
+        pipe.wire_seal(b, frames, foffs)
+        got = records(frames, foffs)
+        for i in range(n):
+            body = oracle.frame_seal(keys[i], nonces[i], msgs[i])
+            assert got[i] == nonces[i] + len(body).to_bytes(4, "big") + body, i
+        frames[int(foffs[9]) + 30] ^= 0x20
+        fb = enet.Batch(frames, foffs, b.keys, b.nonces, total_bytes_hint=int(foffs[-1]),
+                        max_len_hint=max(lens) + 48)
+        back = empty_like(b.arena, pinned)
+        ok = empty_like(torch.zeros(n, dtype=torch.uint8), pinned)
+        pipe.wire_open(fb, back, b.offsets, ok)
+        okh, bk = ok.tolist(), records(back, b.offsets)
+        for i in range(n):
+            assert (okh[i], bk[i]) == ((0, bytes(lens[i])) if i == 9 else (1, msgs[i])), i
+
+
+def test_pipeline_c5_full_per_gpu_share(enet):
+    """BASELINE config 5 at its full per-GPU share -- 65 536 log-uniform
+    512 B-64 KiB records (seed 5, ~0.9 GB) through enet_pipeline_aead_hmac_seal / open from and
+    to pinned host memory.  Every record opens; one tampered tag and one tampered MAC are rejected
+    and their plaintext zeroed; a 256-record sample is bit-exact with the oracle (ciphertext,
+    Poly1305 tag, HMAC-SHA256)."""
+    import torch
+    n = 65536
+    rng = np.random.default_rng(5)
+    lens = np.exp(rng.uniform(np.log(512), np.log(65536), n)).astype(np.int64)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).pin_memory()
+    total = int(offs[-1])
+    g = torch.Generator().manual_seed(55)
+    pt = torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g).pin_memory()
+    keys = torch.randint(0, 256, (32 * n,), dtype=torch.uint8, generator=g).pin_memory()
+    nonces = torch.randint(0, 256, (12 * n,), dtype=torch.uint8, generator=g).pin_memory()
+    ct, back = torch.empty_like(pt).pin_memory(), torch.empty_like(pt).pin_memory()
+    tags = torch.zeros(16 * n, dtype=torch.uint8).pin_memory()
+    macs = torch.zeros(32 * n, dtype=torch.uint8).pin_memory()
+    ok = torch.zeros(n, dtype=torch.uint8).pin_memory()
+    b = enet.Batch(pt, offs, keys, nonces, total_bytes_hint=total, max_len_hint=int(lens.max()))
+    with enet.Pipeline(0) as pipe:
+        pipe.aead_hmac_seal(b, ct, tags, macs)
+        bt, bm = 1234, 40000
+        tags[16 * bt + 7] ^= 0x01
+        macs[32 * bm + 31] ^= 0x80
+        b2 = enet.Batch(ct, offs, keys, nonces, total_bytes_hint=total, max_len_hint=int(lens.max()))
+        pipe.aead_hmac_open(b2, back, tags, macs, ok)
+    okh = ok.numpy()
+    assert [i for i in np.nonzero(okh == 0)[0].tolist()] == [bt, bm]
+    o = offs.numpy()
+    for i in (bt, bm):
+        assert not back[o[i]:o[i + 1]].any(), i
+    pth, cth, bkh = pt.numpy(), ct.numpy(), back.numpy()
+    keep = np.ones(total, dtype=bool)
+    for i in (bt, bm):
+        keep[o[i]:o[i + 1]] = False
+    assert np.array_equal(bkh[keep], pth[keep])
+    kh, nh, th, mh = keys.numpy().tobytes(), nonces.numpy().tobytes(), tags.numpy().tobytes(), macs.numpy().tobytes()
+    sample = sorted(set(np.random.default_rng(6).choice(n, 256, replace=False).tolist()) - {bt, bm})
+    for i in sample:
+        k, v, m = kh[32 * i:32 * i + 32], nh[12 * i:12 * i + 12], pth[o[i]:o[i + 1]].tobytes()
+        c, t = oracle.aead_seal(k, v, m)
+        assert cth[o[i]:o[i + 1]].tobytes() == c and th[16 * i:16 * i + 16] == t, i
+        assert mh[32 * i:32 * i + 32] == oracle.hmac_sha256(k, m), i
