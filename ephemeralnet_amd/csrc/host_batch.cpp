@@ -251,7 +251,9 @@ Mode default_mode() {
     int m = g_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char* e = std::getenv("ENET_HOST_MODE");
-        m = (e && std::strcmp(e, "sdma") == 0) ? (int)Mode::Sdma : (int)Mode::ZeroCopy;
+        m = (e && std::strcmp(e, "sdma") == 0)    ? (int)Mode::Sdma
+            : (e && std::strcmp(e, "split") == 0) ? (int)Mode::SdmaSplit
+                                                  : (int)Mode::ZeroCopy;
         g_mode.store(m, std::memory_order_relaxed);
     }
     return (Mode)m;
@@ -269,9 +271,12 @@ uint32_t worker_threads() {
 }
 
 // ------------------------------------------------------------------------------ engine
+bool via_copies(Mode m) { return m == Mode::Sdma || m == Mode::SdmaSplit; }
+
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t kdone = nullptr;  // SdmaSplit: the chunk's kernel has run (up -> down hand-over)
     Pinned in, out, small;
     DevBuf d_in, d_out, d_small;
     // the chunk in flight
@@ -293,9 +298,14 @@ public:
             Slot& s = *sp;
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.done) (void)hipEventDestroy(s.done);
+            if (s.kdone) (void)hipEventDestroy(s.kdone);
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
         slots_.clear();
+        if (down_) {
+            (void)hipStreamSynchronize(down_);
+            (void)hipStreamDestroy(down_);
+        }
         table_.release();
         mid_.release();
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -314,7 +324,9 @@ private:
             Slot& s = *slots_.back();
             hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
             hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+            hip_check(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming), "hipEventCreate");
         }
+        if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -345,6 +357,7 @@ private:
     Config cfg_;
     mutable std::mutex mu_;
     std::vector<std::unique_ptr<Slot>> slots_;
+    hipStream_t down_ = nullptr;  // SdmaSplit: every D2H
     std::unique_ptr<Pool> pool_;
     EngineStats st_{};
     // per job
@@ -363,7 +376,7 @@ void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b,
     s.lay = layout(j, m);
     const Layout& l = s.lay;
     s.small.ensure(l.total);
-    if (md == Mode::Sdma) {
+    if (via_copies(md)) {
         s.d_small.ensure(l.total);
         s.d_in.ensure(in_b);
         s.d_out.ensure(out_b);
@@ -388,8 +401,7 @@ void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b,
         });
         st_.gathered_bytes += in_b;
     }
-    if (md == Mode::ZeroCopy && !s.direct_out) s.out.ensure(out_b);
-    if (md == Mode::Sdma && !s.direct_out) s.out.ensure(out_b);
+    if (!s.direct_out) s.out.ensure(out_b);
     // ---- small arrays (rebased offsets, keys, nonces, ...)
     uint8_t* sm = s.small.h;
     auto* io = reinterpret_cast<uint64_t*>(sm + l.in_off);
@@ -422,13 +434,14 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     const Mode md = mode();
     const Layout& l = s.lay;
     const uint32_t m = (uint32_t)(s.c1 - s.c0);
-    hipStream_t st = s.stream;
+    // SdmaSplit: H2D + kernel of every chunk on one up stream, D2H on the down stream
+    hipStream_t st = md == Mode::SdmaSplit ? slots_[0]->stream : s.stream;
     // device addresses of this chunk's arenas and small block
     const uint8_t* din;
     uint8_t* dout;
     uint8_t* sm;
     const uint8_t* src_in = in_dev_ ? nullptr : s.in.h;
-    if (md == Mode::Sdma) {
+    if (via_copies(md)) {
         const uint8_t* h_in = in_dev_ ? in_ptr(j, s.c0) : src_in;
         if (in_b) hip_check(hipMemcpyAsync(s.d_in.p, h_in, in_b, hipMemcpyHostToDevice, st), "H2D arena");
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
@@ -487,7 +500,12 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         case Op::ChunkStore: enet_check(enet_chunk_store_batch(&r, ids, macs_out, st), "chunk_store"); break;
         case Op::ChunkFetch: enet_check(enet_chunk_fetch_batch(&r, ids, macs_in, ok, st), "chunk_fetch"); break;
     }
-    if (md == Mode::Sdma) {
+    if (md == Mode::SdmaSplit) {
+        hip_check(hipEventRecord(s.kdone, st), "hipEventRecord");
+        st = down_;
+        hip_check(hipStreamWaitEvent(st, s.kdone, 0), "hipStreamWaitEvent");
+    }
+    if (via_copies(md)) {
         uint8_t* h_out = s.direct_out ? j.out_base + j.out_off[s.c0] : s.out.h;
         if (s.out_b) hip_check(hipMemcpyAsync(h_out, s.d_out.p, s.out_b, hipMemcpyDeviceToHost, st), "D2H arena");
         hip_check(hipMemcpyAsync(s.small.h + l.in_end, s.d_small.p + l.in_end, l.total - l.in_end,
@@ -603,6 +621,8 @@ void Engine::run(const Job& j) {
     uint64_t chunk = cfg_.chunk_bytes;
     if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20))
                                                 : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20));
+    if (!cfg_.chunk_bytes)
+        if (const char* e = std::getenv("ENET_HOST_CHUNK_MIB")) chunk = std::max(1ull, std::strtoull(e, nullptr, 10)) << 20;
     st_.jobs += 1;
     st_.records += n;
     st_.in_bytes += in_total;
@@ -646,6 +666,7 @@ void Engine::run(const Job& j) {
             if (s->stream) (void)hipStreamSynchronize(s->stream);
             s->busy = false;
         }
+        if (down_) (void)hipStreamSynchronize(down_);
         std::rethrow_exception(err);
     }
 }

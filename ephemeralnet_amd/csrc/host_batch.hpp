@@ -73,8 +73,12 @@ struct Job {
 // How the device stage moves the bytes (ENET_HOST_MODE=zc|sdma; enet_host_set_mode):
 //   ZeroCopy -- the kernels read the pinned input and write the pinned output directly over PCIe
 //               (no DMA, no device arenas); both directions move at once inside one launch
-//   Sdma     -- H2D copy into a device arena, kernel, D2H copy back (the copy engines)
-enum class Mode : int { ZeroCopy = 0, Sdma = 1 };
+//   Sdma     -- H2D copy into a device arena, kernel, D2H copy back (the copy engines), each
+//               slot's three steps on that slot's stream
+//   SdmaSplit-- the same copies, but every H2D and kernel on one "up" stream and every D2H on
+//               one "down" stream (an event per slot hands the chunk over), so each copy engine
+//               direction sees back-to-back copies
+enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2 };
 
 struct Config {
     uint64_t chunk_bytes = 0;  // 0: the mode's default

@@ -216,8 +216,10 @@ int main(int argc, char** argv) {
         Host in = host_alloc(T, 0), mid = host_alloc(T, 0), back = host_alloc(T, 0);
         Host tags = host_alloc(16ull * n, 0), ok = host_alloc(n, 0);
         std::memcpy(in.h, pt.data(), T);
+        for (int mode : {0, 1, 2})
         for (uint32_t streams : {3u, 2u, 4u}) {
-            for (uint64_t chunk : {16ull << 20, 64ull << 20}) {
+            for (uint64_t chunk : {0ull, 16ull << 20, 64ull << 20}) {
+                if (enet_host_set_mode(mode)) { std::fprintf(stderr, "mode %d: %s\n", mode, enet_last_error()); return 5; }
                 enet_pipeline* p = enet_pipeline_create(0, chunk, streams);
                 enet_records r{};
                 r.count = n;
@@ -240,8 +242,8 @@ int main(int argc, char** argv) {
                 uint64_t good = 0;
                 for (uint32_t i = 0; i < n; ++i) good += ok.h[i];
                 if (good != n || std::memcmp(back.h, pt.data(), T)) { std::fprintf(stderr, "pipe FAILED\n"); return 4; }
-                std::printf("{\"case\":\"pipe\",\"streams\":%u,\"chunk_mib\":%llu,\"seal_GiBs\":%.2f,\"open_GiBs\":%.2f,"
-                            "\"seal_open_GiBs\":%.2f}\n", streams, (unsigned long long)(chunk >> 20),
+                std::printf("{\"case\":\"pipe\",\"mode\":%d,\"streams\":%u,\"chunk_mib\":%llu,\"seal_GiBs\":%.2f,\"open_GiBs\":%.2f,"
+                            "\"seal_open_GiBs\":%.2f}\n", mode, streams, (unsigned long long)(chunk >> 20),
                             gib((t1 - t0) / reps), gib((t2 - t1) / reps), gib((t2 - t0) / reps));
                 std::fflush(stdout);
                 enet_pipeline_destroy(p);
