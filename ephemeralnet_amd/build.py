@@ -67,7 +67,10 @@ def source_digest(tools: bool = False) -> str:
     """SHA-256 over the compiler, the flags and the bytes of every source and header the library
     is built from (csrc/ and include/): what the built .so claims to be in its stamp file."""
     h = hashlib.sha256()
-    h.update(" ".join([HIPCC] + CFLAGS + LDFLAGS + (["-DENET_TOOLS_BUILD"] if tools else [])).encode())
+    # flags with the checkout's absolute include path made relative: the GPU box runs the same
+    # tree from another directory and must compute the same digest
+    flags = [f.replace(ROOT, ".") for f in CFLAGS + LDFLAGS] + (["-DENET_TOOLS_BUILD"] if tools else [])
+    h.update(" ".join([os.path.basename(HIPCC)] + flags).encode())
     files = [os.path.join(CSRC, f) for f in SOURCES] + _headers()
     for f in sorted(set(files)):
         h.update(os.path.relpath(f, ROOT).encode() + b"\0")

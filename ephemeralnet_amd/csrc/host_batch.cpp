@@ -561,11 +561,11 @@ void Engine::run(const Job& j) {
     const size_t n = j.n;
     if (n == 0) return;
     if (n > 0xFFFFFFFFull) throw std::invalid_argument("enet host batch: more than 2^32 - 1 records");
-    if (!j.in_spans.empty() ? j.in_spans.size() != n : (!j.in_base || !j.in_off))
+    if (!j.in_spans.empty() ? j.in_spans.size() != n : !j.in_off)
         throw std::invalid_argument("enet host batch: input records missing");
     const bool vec_out = j.out_vecs || !j.out_each.empty();
     if (!j.out_each.empty() && j.out_each.size() != n) throw std::invalid_argument("enet host batch: out_each size");
-    if (!vec_out && (!j.out_base || !j.out_off)) throw std::invalid_argument("enet host batch: output missing");
+    if (!vec_out && !j.out_off) throw std::invalid_argument("enet host batch: output offsets missing");
     if (!j.keys) throw std::invalid_argument("enet host batch: keys missing");
     if (j.key_stride != 0 && j.key_stride != 32) throw std::invalid_argument("enet host batch: key_stride must be 0 or 32");
     if (!j.nonces && j.op != Op::WireOpen) throw std::invalid_argument("enet host batch: nonces missing");
@@ -600,6 +600,8 @@ void Engine::run(const Job& j) {
         if (!vec_out && j.out_off[i + 1] - j.out_off[i] != lout_[i])
             throw std::invalid_argument("enet host batch: output offsets do not give the op's output lengths");
     }
+    if (!vec_out && !j.out_base && out_total) throw std::invalid_argument("enet host batch: output arena missing");
+    if (j.in_spans.empty() && !j.in_base && in_total) throw std::invalid_argument("enet host batch: input arena missing");
     if (j.out_vecs) j.out_vecs->resize(n);
     // in place where the caller's arenas are device-accessible
     in_dev_ = j.in_spans.empty() ? device_view(j.in_base + j.in_off[0], in_total) : nullptr;
