@@ -253,6 +253,7 @@ Mode default_mode() {
         const char* e = std::getenv("ENET_HOST_MODE");
         m = (e && std::strcmp(e, "sdma") == 0)    ? (int)Mode::Sdma
             : (e && std::strcmp(e, "split") == 0) ? (int)Mode::SdmaSplit
+            : (e && std::strcmp(e, "splitk") == 0) ? (int)Mode::SdmaSplitK
                                                   : (int)Mode::ZeroCopy;
         g_mode.store(m, std::memory_order_relaxed);
     }
@@ -271,12 +272,14 @@ uint32_t worker_threads() {
 }
 
 // ------------------------------------------------------------------------------ engine
-bool via_copies(Mode m) { return m == Mode::Sdma || m == Mode::SdmaSplit; }
+bool via_copies(Mode m) { return m != Mode::ZeroCopy; }
+bool split_dirs(Mode m) { return m == Mode::SdmaSplit || m == Mode::SdmaSplitK; }
 
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
-    hipEvent_t kdone = nullptr;  // SdmaSplit: the chunk's kernel has run (up -> down hand-over)
+    hipEvent_t kdone = nullptr;   // SdmaSplit*: the chunk's kernel has run (-> down stream)
+    hipEvent_t indone = nullptr;  // SdmaSplitK: the chunk's H2D copies are done (-> slot stream)
     Pinned in, out, small;
     DevBuf d_in, d_out, d_small;
     // the chunk in flight
@@ -299,13 +302,15 @@ public:
             if (s.stream) (void)hipStreamSynchronize(s.stream);
             if (s.done) (void)hipEventDestroy(s.done);
             if (s.kdone) (void)hipEventDestroy(s.kdone);
+            if (s.indone) (void)hipEventDestroy(s.indone);
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
         slots_.clear();
-        if (down_) {
-            (void)hipStreamSynchronize(down_);
-            (void)hipStreamDestroy(down_);
-        }
+        for (hipStream_t x : {up_, down_})
+            if (x) {
+                (void)hipStreamSynchronize(x);
+                (void)hipStreamDestroy(x);
+            }
         table_.release();
         mid_.release();
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -325,8 +330,12 @@ private:
             hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
             hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
             hip_check(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming), "hipEventCreate");
+            hip_check(hipEventCreateWithFlags(&s.indone, hipEventDisableTiming), "hipEventCreate");
         }
-        if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
+        if (split_dirs(mode())) {
+            if (!up_) hip_check(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking), "hipStreamCreate");
+            if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
+        }
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -357,7 +366,8 @@ private:
     Config cfg_;
     mutable std::mutex mu_;
     std::vector<std::unique_ptr<Slot>> slots_;
-    hipStream_t down_ = nullptr;  // SdmaSplit: every D2H
+    hipStream_t up_ = nullptr;    // SdmaSplit*: every H2D (and SdmaSplit: every kernel)
+    hipStream_t down_ = nullptr;  // SdmaSplit*: every D2H
     std::unique_ptr<Pool> pool_;
     EngineStats st_{};
     // per job
@@ -434,8 +444,9 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     const Mode md = mode();
     const Layout& l = s.lay;
     const uint32_t m = (uint32_t)(s.c1 - s.c0);
-    // SdmaSplit: H2D + kernel of every chunk on one up stream, D2H on the down stream
-    hipStream_t st = md == Mode::SdmaSplit ? slots_[0]->stream : s.stream;
+    // SdmaSplit: H2D + kernel of every chunk on the up stream, D2H on the down stream;
+    // SdmaSplitK: H2D on up, kernel on the slot's stream, D2H on down
+    hipStream_t st = split_dirs(md) ? up_ : s.stream;
     // device addresses of this chunk's arenas and small block
     const uint8_t* din;
     uint8_t* dout;
@@ -445,6 +456,11 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         const uint8_t* h_in = in_dev_ ? in_ptr(j, s.c0) : src_in;
         if (in_b) hip_check(hipMemcpyAsync(s.d_in.p, h_in, in_b, hipMemcpyHostToDevice, st), "H2D arena");
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
+        if (md == Mode::SdmaSplitK) {
+            hip_check(hipEventRecord(s.indone, st), "hipEventRecord");
+            st = s.stream;
+            hip_check(hipStreamWaitEvent(st, s.indone, 0), "hipStreamWaitEvent");
+        }
         din = s.d_in.p;
         dout = s.d_out.p;
         sm = s.d_small.p;
@@ -500,7 +516,7 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         case Op::ChunkStore: enet_check(enet_chunk_store_batch(&r, ids, macs_out, st), "chunk_store"); break;
         case Op::ChunkFetch: enet_check(enet_chunk_fetch_batch(&r, ids, macs_in, ok, st), "chunk_fetch"); break;
     }
-    if (md == Mode::SdmaSplit) {
+    if (split_dirs(md)) {
         hip_check(hipEventRecord(s.kdone, st), "hipEventRecord");
         st = down_;
         hip_check(hipStreamWaitEvent(st, s.kdone, 0), "hipStreamWaitEvent");
@@ -545,9 +561,8 @@ void Engine::finish(Slot& s, const Job& j) {
         for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
             const uint64_t len = lout_[i];
             if (j.out_vecs || !j.out_each.empty()) {
-                auto& v = vec_of(j, i);
-                v.resize(len);
-                if (len) std::memcpy(v.data(), base + r, len);
+                // assign from the range: one allocation and one copy, no zero fill first
+                vec_of(j, i).assign(base + r, base + r + len);
             } else if (len) {
                 std::memcpy(j.out_base + j.out_off[i], base + r, len);
             }
@@ -668,7 +683,8 @@ void Engine::run(const Job& j) {
             if (s->stream) (void)hipStreamSynchronize(s->stream);
             s->busy = false;
         }
-        if (down_) (void)hipStreamSynchronize(down_);
+        for (hipStream_t x : {up_, down_})
+            if (x) (void)hipStreamSynchronize(x);
         std::rethrow_exception(err);
     }
 }

@@ -78,7 +78,10 @@ struct Job {
 //   SdmaSplit-- the same copies, but every H2D and kernel on one "up" stream and every D2H on
 //               one "down" stream (an event per slot hands the chunk over), so each copy engine
 //               direction sees back-to-back copies
-enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2 };
+//   SdmaSplitK -- H2D on the up stream, the kernel on the chunk's slot stream (kernels of
+//               consecutive chunks may overlap: mixed batches whose serial HMAC chains outlast a
+//               chunk's copies), D2H on the down stream
+enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2, SdmaSplitK = 3 };
 
 struct Config {
     uint64_t chunk_bytes = 0;  // 0: the mode's default
