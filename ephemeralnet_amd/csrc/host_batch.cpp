@@ -23,6 +23,8 @@
 #include <thread>
 #include <vector>
 
+#include <immintrin.h>
+
 #include "enet_crypto.h"
 
 namespace enet::hb {
@@ -120,6 +122,45 @@ private:
     uint64_t gen_ = 0;
     bool stop_ = false;
 };
+
+// ------------------------------------------------------------------------------ streaming copy
+// Gather / scatter copies move every record once between the caller's memory and the pinned
+// staging, while the copy engines read / write that staging too.  Non-temporal (streaming)
+// stores skip the read-for-ownership of the destination lines and keep the copies out of the
+// caches the session threads use; ENET_HOST_NT=0 selects plain memcpy.  The caller issues a store
+// fence before the staging is handed to the device (fence_stores).
+__attribute__((target("avx512f"))) void copy_nt512(uint8_t* d, const uint8_t* s, size_t n) {
+    const size_t head = std::min<size_t>(n, (64 - (reinterpret_cast<uintptr_t>(d) & 63)) & 63);
+    std::memcpy(d, s, head);
+    d += head;
+    s += head;
+    n -= head;
+    for (; n >= 256; n -= 256, d += 256, s += 256) {
+        const __m512i a = _mm512_loadu_si512(s), b = _mm512_loadu_si512(s + 64), c = _mm512_loadu_si512(s + 128),
+                      e = _mm512_loadu_si512(s + 192);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(d), a);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(d + 64), b);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(d + 128), c);
+        _mm512_stream_si512(reinterpret_cast<__m512i*>(d + 192), e);
+    }
+    for (; n >= 64; n -= 64, d += 64, s += 64) _mm512_stream_si512(reinterpret_cast<__m512i*>(d), _mm512_loadu_si512(s));
+    std::memcpy(d, s, n);
+}
+
+bool use_nt() {
+    static const bool v = [] {
+        const char* e = std::getenv("ENET_HOST_NT");
+        return !(e && e[0] == '0') && __builtin_cpu_supports("avx512f");
+    }();
+    return v;
+}
+
+void copy_out(uint8_t* d, const uint8_t* s, size_t n) {
+    if (n >= 512 && use_nt()) copy_nt512(d, s, n);
+    else if (n) std::memcpy(d, s, n);
+}
+
+void fence_stores() { _mm_sfence(); }
 
 // ------------------------------------------------------------------------------ buffers
 struct Pinned {  // pinned, device-mapped host memory, grow-only
@@ -405,9 +446,10 @@ void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b,
         pool().parallel(cut.size() - 1, [&](size_t p) {
             uint64_t w = at[p];
             for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
-                if (lin_[i]) std::memcpy(base + w, in_ptr(j, i), lin_[i]);
+                copy_out(base + w, in_ptr(j, i), lin_[i]);
                 w += lin_[i];
             }
+            fence_stores();  // the streamed lines are globally visible before the device reads them
         });
         st_.gathered_bytes += in_b;
     }
@@ -563,11 +605,12 @@ void Engine::finish(Slot& s, const Job& j) {
             if (j.out_vecs || !j.out_each.empty()) {
                 // assign from the range: one allocation and one copy, no zero fill first
                 vec_of(j, i).assign(base + r, base + r + len);
-            } else if (len) {
-                std::memcpy(j.out_base + j.out_off[i], base + r, len);
+            } else {
+                copy_out(j.out_base + j.out_off[i], base + r, len);
             }
             r += len;
         }
+        fence_stores();
     });
     st_.scattered_bytes += s.out_b;
 }

@@ -28,11 +28,10 @@ for l in open('$O/host.jsonl'):
     d=json.loads(l); c=d['config']; print(d['mode'], c.get('workload','C2'), c.get('chunk_mib', c.get('c5_chunk_mib')), d['value'])"
 step batch_bench
 : > $O/batch.jsonl
-for m in split zc; do
-  for th in 8 15; do
-    ENET_HOST_MODE=$m ENET_HOST_THREADS=$th timeout -k 10 300 tools/batch_bench all 3 > $O/x.jsonl 2>> $O/batch.err || { echo "batch $m $th failed"; exit 1; }
-    sed "s/^{/{\"mode\":\"$m\",\"threads\":$th,/" $O/x.jsonl >> $O/batch.jsonl
-  done
+for cfg in "split 8 1" "split 15 1" "split 15 0" "zc 15 1"; do
+  set -- $cfg
+  ENET_HOST_MODE=$1 ENET_HOST_THREADS=$2 ENET_HOST_NT=$3 timeout -k 10 300 tools/batch_bench all 3 > $O/x.jsonl 2>> $O/batch.err || { echo "batch $cfg failed"; exit 1; }
+  sed "s/^{/{\"mode\":\"$1\",\"threads\":$2,\"nt\":$3,/" $O/x.jsonl >> $O/batch.jsonl
 done
 cat $O/batch.jsonl
 step done
