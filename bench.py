@@ -267,6 +267,35 @@ def cpu_reference_frames(record_bytes: int, budget_s: float) -> dict | None:
                       f"ChaCha20, oracle/_ref compiled from src/crypto), {threads} threads"}
 
 
+_PINNED = []  # enet_host_alloc blocks of this process (freed at exit by the OS)
+
+
+def pinned_empty(nbytes: int):
+    """A uint8 CPU tensor over pinned host memory from the library's allocator (enet_host_alloc =
+    hipHostMalloc), the buffer pools INTEGRATION.md gives socket / relay code."""
+    import ctypes as C
+
+    import torch
+
+    import ephemeralnet_amd as E
+    p = E.lib().enet_host_alloc(max(nbytes, 1))
+    if not p:
+        raise SystemExit("enet_host_alloc failed")
+    _PINNED.append(p)
+    return torch.frombuffer((C.c_uint8 * max(nbytes, 1)).from_address(p), dtype=torch.uint8)[:nbytes]
+
+
+def pinned_copy(t):
+    out = pinned_empty(t.numel() * t.element_size())
+    out.copy_(t.contiguous().view(-1).view(torch_uint8()))
+    return out
+
+
+def torch_uint8():
+    import torch
+    return torch.uint8
+
+
 def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, streams: int = 0) -> dict:
     """C2 shape starting and ending in pinned host memory (the reference's socket / relay path),
     through the library's host pipeline (enet_pipeline_aead_*, host_batch.cpp runtime): seal then
@@ -277,14 +306,14 @@ def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, s
     import ephemeralnet_amd as E
 
     g = torch.Generator().manual_seed(7)
-    pt_h = torch.randint(0, 256, (n * L,), dtype=torch.uint8, generator=g).pin_memory()
-    keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
-    nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
-    offs_h = torch.arange(0, (n + 1) * L, L, dtype=torch.int64).pin_memory()
-    ct_h = torch.empty_like(pt_h).pin_memory()
-    back_h = torch.empty_like(pt_h).pin_memory()
-    tags_h = torch.empty(16 * n, dtype=torch.uint8).pin_memory()
-    ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    pt_h = pinned_copy(torch.randint(0, 256, (n * L,), dtype=torch.uint8, generator=g))
+    keys_h = pinned_copy(torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g))
+    nonces_h = pinned_copy(torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g))
+    offs_h = pinned_copy(torch.arange(0, (n + 1) * L, L, dtype=torch.int64)).view(torch.int64)
+    ct_h = pinned_empty(n * L)
+    back_h = pinned_empty(n * L)
+    tags_h = pinned_empty(16 * n)
+    ok_h = pinned_empty(n)
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=n * L, max_len_hint=L)
     pipe = E.Pipeline(dev_index, chunk_mib << 20, streams)
@@ -429,17 +458,17 @@ def host_c5_rank(dev_index: int, lens, seed: int, chunk_mib: int, streams: int, 
     import ephemeralnet_amd as E
 
     n = len(lens)
-    offs_h = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).pin_memory()
+    offs_h = pinned_copy(torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))).view(torch.int64)
     total = int(offs_h[-1])
     g = torch.Generator().manual_seed(seed)
-    pt_h = torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g).pin_memory()
-    keys_h = torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g).pin_memory()
-    nonces_h = torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g).pin_memory()
-    ct_h = torch.empty_like(pt_h).pin_memory()
-    back_h = torch.empty_like(pt_h).pin_memory()
-    tags_h = torch.empty(16 * n, dtype=torch.uint8).pin_memory()
-    macs_h = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
-    ok_h = torch.empty(n, dtype=torch.uint8).pin_memory()
+    pt_h = pinned_copy(torch.randint(0, 256, (total,), dtype=torch.uint8, generator=g))
+    keys_h = pinned_copy(torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g))
+    nonces_h = pinned_copy(torch.randint(0, 256, (n * 12,), dtype=torch.uint8, generator=g))
+    ct_h = pinned_empty(total)
+    back_h = pinned_empty(total)
+    tags_h = pinned_empty(16 * n)
+    macs_h = pinned_empty(32 * n)
+    ok_h = pinned_empty(n)
     mx = int(lens.max()) if n else 0
     seal_b = E.Batch(pt_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)
     open_b = E.Batch(ct_h, offs_h, keys_h, nonces_h, total_bytes_hint=total, max_len_hint=mx)

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -314,6 +316,18 @@ uint32_t worker_threads() {
 
 // ------------------------------------------------------------------------------ engine
 bool via_copies(Mode m) { return m != Mode::ZeroCopy; }
+
+// ENET_HOST_TRACE=1: one stderr line per job with where its wall time went (tuning)
+bool trace_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("ENET_HOST_TRACE");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 bool split_dirs(Mode m) { return m == Mode::SdmaSplit || m == Mode::SdmaSplitK; }
 
 struct Slot {
@@ -416,6 +430,7 @@ private:
     uint8_t* out_dev_ = nullptr;        // ... output arena (direct out)
     std::vector<uint64_t> lin_, lout_;  // record lengths in / out
     DevBuf table_, mid_;                // session key table + HMAC midstates on the device
+    double t_wait_ = 0, t_scatter_ = 0, t_gather_ = 0, t_launch_ = 0;  // ENET_HOST_TRACE
     const uint8_t* in_ptr(const Job& j, size_t i) const {
         return j.in_spans.empty() ? j.in_base + j.in_off[i] : j.in_spans[i].data();
     }
@@ -575,7 +590,15 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
 
 void Engine::finish(Slot& s, const Job& j) {
     s.busy = false;
+    const double t0 = now_s();
     hip_check(hipEventSynchronize(s.done), "chunk sync");
+    const double t1 = now_s();
+    t_wait_ += t1 - t0;
+    struct Acc {
+        double& acc;
+        double t;
+        ~Acc() { acc += now_s() - t; }
+    } acc{t_scatter_, t1};
     const size_t c0 = s.c0, c1 = s.c1;
     const uint32_t m = (uint32_t)(c1 - c0);
     const Layout& l = s.lay;
@@ -640,7 +663,11 @@ void Engine::run(const Job& j) {
     } restore{prev, dev_};
 
     const Mode md = mode();
-    const uint32_t S = cfg_.slots ? std::min<uint32_t>(cfg_.slots, 8) : 3u;
+    static const uint32_t env_slots = [] {
+        const char* e = std::getenv("ENET_HOST_SLOTS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    const uint32_t S = std::min<uint32_t>(cfg_.slots ? cfg_.slots : env_slots ? env_slots : 3u, 8);
     setup_slots(S);
     // lengths
     const int64_t delta = delta_of(j.op);
@@ -689,6 +716,8 @@ void Engine::run(const Job& j) {
     st_.out_bytes += out_total;
     size_t c0 = 0, k = 0;
     std::exception_ptr err;
+    t_wait_ = t_scatter_ = t_gather_ = t_launch_ = 0;
+    const double t_job = now_s();
     try {
         while (c0 < n) {
             size_t c1 = c0 + 1;
@@ -707,8 +736,12 @@ void Engine::run(const Job& j) {
             s.c1 = c1;
             s.out_b = ob;
             s.direct_out = direct_out;
+            const double t0 = now_s();
             prepare(s, j, c0, c1, ib, ob, mx);
+            const double t1 = now_s();
             launch(s, j, ib, mx, ib != (uint64_t)(c1 - c0) * mx);
+            t_gather_ += t1 - t0;
+            t_launch_ += now_s() - t1;
             st_.chunks += 1;
             if (in_dev_) st_.direct_in += 1;
             if (direct_out) st_.direct_out += 1;
@@ -721,6 +754,13 @@ void Engine::run(const Job& j) {
     } catch (...) {
         err = std::current_exception();
     }
+    if (trace_on())
+        std::fprintf(stderr,
+                     "[enet host] op %d mode %d n %zu in %llu out %llu chunks %zu slots %u: total %.3f ms = "
+                     "gather+small %.3f, launch %.3f, wait %.3f, scatter+small %.3f ms (direct in %d out %d)\n",
+                     (int)j.op, (int)md, n, (unsigned long long)in_total, (unsigned long long)out_total, k, S,
+                     1e3 * (now_s() - t_job), 1e3 * t_gather_, 1e3 * t_launch_, 1e3 * t_wait_, 1e3 * t_scatter_,
+                     in_dev_ != nullptr, (int)direct_out);
     if (err) {  // drain whatever is still in flight before the caller's buffers go away
         for (auto& s : slots_) {
             if (s->stream) (void)hipStreamSynchronize(s->stream);
