@@ -285,6 +285,15 @@ def pinned_empty(nbytes: int):
     return torch.frombuffer((C.c_uint8 * max(nbytes, 1)).from_address(p), dtype=torch.uint8)[:nbytes]
 
 
+def pinned_release(mark: int) -> None:
+    """Free the enet_host_alloc blocks taken since len(_PINNED) was `mark` (their tensors must be
+    dead by now)."""
+    import ephemeralnet_amd as E
+    E.lib().enet_host_free.argtypes = [__import__("ctypes").c_void_p]
+    while len(_PINNED) > mark:
+        E.lib().enet_host_free(_PINNED.pop())
+
+
 def pinned_copy(t):
     out = pinned_empty(t.numel() * t.element_size())
     out.copy_(t.contiguous().view(-1).view(torch_uint8()))
@@ -305,6 +314,7 @@ def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, s
 
     import ephemeralnet_amd as E
 
+    mark = len(_PINNED)
     g = torch.Generator().manual_seed(7)
     pt_h = pinned_copy(torch.randint(0, 256, (n * L,), dtype=torch.uint8, generator=g))
     keys_h = pinned_copy(torch.randint(0, 256, (n * 32,), dtype=torch.uint8, generator=g))
@@ -327,7 +337,10 @@ def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, s
         pipe.aead_open(open_b, back_h, tags_h, ok_h)
     t2 = time.perf_counter()
     pipe.close()
-    if int(ok_h.sum()) != n or not torch.equal(back_h, pt_h):
+    good = int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
+    del pt_h, keys_h, nonces_h, offs_h, ct_h, back_h, tags_h, ok_h, seal_b, open_b
+    pinned_release(mark)
+    if not good:
         raise SystemExit("host-resident C2: round trip failed")
     gib = n * L * reps / 2**30
     return {"gibs": gib / (t2 - t0), "seal_gibs": gib / (t1 - t0), "open_gibs": gib / (t2 - t1)}
@@ -458,6 +471,7 @@ def host_c5_rank(dev_index: int, lens, seed: int, chunk_mib: int, streams: int, 
     import ephemeralnet_amd as E
 
     n = len(lens)
+    mark = len(_PINNED)
     offs_h = pinned_copy(torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64))).view(torch.int64)
     total = int(offs_h[-1])
     g = torch.Generator().manual_seed(seed)
@@ -479,8 +493,12 @@ def host_c5_rank(dev_index: int, lens, seed: int, chunk_mib: int, streams: int, 
         pipe.aead_hmac_open(open_b, back_h, tags_h, macs_h, ok_h)
 
     def check():
+        nonlocal pt_h, back_h, ct_h
         good = int(ok_h.sum()) == n and torch.equal(back_h, pt_h)
         pipe.close()
+        pt_h = back_h = ct_h = None
+        seal_b.arena = open_b.arena = None
+        pinned_release(mark)
         return good
 
     return step, check, total
