@@ -53,6 +53,7 @@ public:
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
+            pub_stop_ = true;
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -70,6 +71,7 @@ public:
             std::lock_guard<std::mutex> lk(mu_);
             task_ = &t;
             ++gen_;
+            pub_gen_.store(gen_, std::memory_order_release);
         }
         cv_.notify_all();
         work(t);
@@ -106,6 +108,15 @@ private:
         uint64_t seen = 0;
         std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
+            if (!stop_ && !(task_ && gen_ != seen)) {
+                // a pipeline hands out a task set every few hundred microseconds: spin ~20 us for
+                // the next one before sleeping (a futex wake-up per worker per set cost ~1.5 ms per
+                // 256 MiB job)
+                lk.unlock();
+                for (int i = 0; i < 4000 && pub_gen_.load(std::memory_order_acquire) == seen && !pub_stop_.load(); ++i)
+                    _mm_pause();
+                lk.lock();
+            }
             cv_.wait(lk, [&] { return stop_ || (task_ && gen_ != seen); });
             if (stop_) return;
             seen = gen_;
@@ -123,6 +134,8 @@ private:
     Task* task_ = nullptr;
     uint64_t gen_ = 0;
     bool stop_ = false;
+    std::atomic<uint64_t> pub_gen_{0};  // gen_ for the spinning workers
+    std::atomic<bool> pub_stop_{false};
 };
 
 // ------------------------------------------------------------------------------ streaming copy
@@ -413,9 +426,18 @@ private:
         cut.push_back(b);
         return cut;
     }
-    void prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b, uint32_t mx);
+    struct CopyTask {
+        int kind;  // 0 gather records [a, b) into base + at; 1 scatter them from base + at
+        Slot* s;
+        size_t a, b;
+        uint64_t at;
+        uint8_t* base;
+    };
+    void stage(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b, std::vector<CopyTask>& tasks);
+    void fill(Slot& s, const Job& j, uint64_t in_b, uint64_t out_b, uint32_t mx);
+    void run_tasks(const Job& j, std::vector<CopyTask>& tasks);
     void launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixed);
-    void finish(Slot& s, const Job& j);
+    void retire(Slot& s, const Job& j, std::vector<CopyTask>& tasks);
 
     int dev_;
     Config cfg_;
@@ -430,46 +452,43 @@ private:
     uint8_t* out_dev_ = nullptr;        // ... output arena (direct out)
     std::vector<uint64_t> lin_, lout_;  // record lengths in / out
     DevBuf table_, mid_;                // session key table + HMAC midstates on the device
-    double t_wait_ = 0, t_scatter_ = 0, t_gather_ = 0, t_launch_ = 0;  // ENET_HOST_TRACE
+    double t_wait_ = 0, t_copy_ = 0, t_fill_ = 0, t_launch_ = 0;  // ENET_HOST_TRACE
     const uint8_t* in_ptr(const Job& j, size_t i) const {
         return j.in_spans.empty() ? j.in_base + j.in_off[i] : j.in_spans[i].data();
     }
 };
 
-void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b, uint32_t mx) {
+// Stage a chunk into slot s: layout and device buffers, and the gather tasks that copy its
+// records into the pinned input arena (run by run_tasks, together with the previous chunk's scatter)
+void Engine::stage(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, uint64_t out_b,
+                   std::vector<CopyTask>& tasks) {
     const uint32_t m = (uint32_t)(c1 - c0);
     const Mode md = mode();
     s.lay = layout(j, m);
-    const Layout& l = s.lay;
-    s.small.ensure(l.total);
+    s.small.ensure(s.lay.total);
     if (via_copies(md)) {
-        s.d_small.ensure(l.total);
+        s.d_small.ensure(s.lay.total);
         s.d_in.ensure(in_b);
         s.d_out.ensure(out_b);
     }
-    // ---- inputs: gather the records into the pinned arena (unless the caller's is usable)
-    if (!in_dev_) {
-        s.in.ensure(in_b);
-        uint8_t* base = s.in.h;
-        const auto cut = split(c0, c1, in_b, [&](size_t i) { return lin_[i]; });
-        std::vector<uint64_t> at(cut.size());
-        uint64_t o = 0;
-        for (size_t p = 0, i = c0; p + 1 < cut.size(); ++p) {
-            at[p] = o;
-            for (; i < cut[p + 1]; ++i) o += lin_[i];
-        }
-        pool().parallel(cut.size() - 1, [&](size_t p) {
-            uint64_t w = at[p];
-            for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
-                copy_out(base + w, in_ptr(j, i), lin_[i]);
-                w += lin_[i];
-            }
-            fence_stores();  // the streamed lines are globally visible before the device reads them
-        });
-        st_.gathered_bytes += in_b;
+    if (in_dev_) return;  // the caller's input arena is device-accessible: used in place
+    s.in.ensure(in_b);
+    const auto cut = split(c0, c1, in_b, [&](size_t i) { return lin_[i]; });
+    uint64_t o = 0;
+    for (size_t p = 0, i = c0; p + 1 < cut.size(); ++p) {
+        tasks.push_back({0, &s, cut[p], cut[p + 1], o, s.in.h});
+        for (; i < cut[p + 1]; ++i) o += lin_[i];
     }
+    st_.gathered_bytes += in_b;
+}
+
+// The per-record small arrays of the chunk in slot s (rebased offsets, keys, nonces, ...) and its
+// output staging; after run_tasks, so the previous chunk's scatter has read the old staging
+void Engine::fill(Slot& s, const Job& j, uint64_t in_b, uint64_t out_b, uint32_t mx) {
+    const size_t c0 = s.c0;
+    const uint32_t m = (uint32_t)(s.c1 - s.c0);
+    const Layout& l = s.lay;
     if (!s.direct_out) s.out.ensure(out_b);
-    // ---- small arrays (rebased offsets, keys, nonces, ...)
     uint8_t* sm = s.small.h;
     auto* io = reinterpret_cast<uint64_t*>(sm + l.in_off);
     auto* oo = reinterpret_cast<uint64_t*>(sm + l.out_off);
@@ -495,6 +514,34 @@ void Engine::prepare(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b,
         const uint64_t* len = lin_.data() + c0;
         std::stable_sort(ord, ord + m, [len](uint32_t a, uint32_t b) { return len[a] > len[b]; });
     }
+}
+
+// Gather and scatter parts of (up to) two chunks in one pool pass: independent memory streams
+void Engine::run_tasks(const Job& j, std::vector<CopyTask>& tasks) {
+    if (tasks.empty()) return;
+    pool().parallel(tasks.size(), [&](size_t t) {
+        const CopyTask& c = tasks[t];
+        uint64_t o = c.at;
+        if (c.kind == 0) {
+            for (size_t i = c.a; i < c.b; ++i) {
+                copy_out(c.base + o, in_ptr(j, i), lin_[i]);
+                o += lin_[i];
+            }
+        } else {
+            for (size_t i = c.a; i < c.b; ++i) {
+                const uint64_t len = lout_[i];
+                if (j.out_vecs || !j.out_each.empty()) {
+                    // assign from the range: one allocation and one copy, no zero fill first
+                    vec_of(j, i).assign(c.base + o, c.base + o + len);
+                } else {
+                    copy_out(j.out_base + j.out_off[i], c.base + o, len);
+                }
+                o += len;
+            }
+        }
+        fence_stores();  // streamed lines are globally visible before the device / caller reads them
+    });
+    tasks.clear();
 }
 
 void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixed) {
@@ -588,17 +635,13 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     s.busy = true;
 }
 
-void Engine::finish(Slot& s, const Job& j) {
+// The chunk in slot s is done on the device: wait for it, copy its small outputs, and queue the
+// scatter of its records (run by run_tasks)
+void Engine::retire(Slot& s, const Job& j, std::vector<CopyTask>& tasks) {
     s.busy = false;
     const double t0 = now_s();
     hip_check(hipEventSynchronize(s.done), "chunk sync");
-    const double t1 = now_s();
-    t_wait_ += t1 - t0;
-    struct Acc {
-        double& acc;
-        double t;
-        ~Acc() { acc += now_s() - t; }
-    } acc{t_scatter_, t1};
+    t_wait_ += now_s() - t0;
     const size_t c0 = s.c0, c1 = s.c1;
     const uint32_t m = (uint32_t)(c1 - c0);
     const Layout& l = s.lay;
@@ -613,28 +656,12 @@ void Engine::finish(Slot& s, const Job& j) {
             for (size_t i = c0; i < c1; ++i) vec_of(j, i).clear();
         return;
     }
-    const uint8_t* base = s.out.h;
     const auto cut = split(c0, c1, s.out_b, [&](size_t i) { return lout_[i]; });
-    std::vector<uint64_t> at(cut.size());
     uint64_t o = 0;
     for (size_t p = 0, i = c0; p + 1 < cut.size(); ++p) {
-        at[p] = o;
+        tasks.push_back({1, &s, cut[p], cut[p + 1], o, s.out.h});
         for (; i < cut[p + 1]; ++i) o += lout_[i];
     }
-    pool().parallel(cut.size() - 1, [&](size_t p) {
-        uint64_t r = at[p];
-        for (size_t i = cut[p]; i < cut[p + 1]; ++i) {
-            const uint64_t len = lout_[i];
-            if (j.out_vecs || !j.out_each.empty()) {
-                // assign from the range: one allocation and one copy, no zero fill first
-                vec_of(j, i).assign(base + r, base + r + len);
-            } else {
-                copy_out(j.out_base + j.out_off[i], base + r, len);
-            }
-            r += len;
-        }
-        fence_stores();
-    });
     st_.scattered_bytes += s.out_b;
 }
 
@@ -716,32 +743,46 @@ void Engine::run(const Job& j) {
     st_.out_bytes += out_total;
     size_t c0 = 0, k = 0;
     std::exception_ptr err;
-    t_wait_ = t_scatter_ = t_gather_ = t_launch_ = 0;
+    t_wait_ = t_copy_ = t_fill_ = t_launch_ = 0;
     const double t_job = now_s();
+    std::vector<CopyTask> tasks;
+    uint64_t left = in_total;
     try {
         while (c0 < n) {
+            // ramped chunk sizes: the first chunks (nothing to overlap their copy in yet) and
+            // the last ones (nothing left to overlap their copy out) are small, 1/8 .. 1/2 of the
+            // steady chunk, so the pipeline fills and drains in a fraction of a chunk's time
+            uint64_t target = chunk;
+            if (k < 3) target = std::max<uint64_t>(chunk >> (3 - k), 1);
+            if (left < 2 * chunk) target = std::min<uint64_t>(target, std::max<uint64_t>(left / 2, chunk >> 3));
             size_t c1 = c0 + 1;
             uint64_t ib = lin_[c0], ob = lout_[c0];
             uint32_t mx = (uint32_t)std::min<uint64_t>(lin_[c0], 0xFFFFFFFFu);
-            while (c1 < n && ib + lin_[c1] <= chunk && ob + lout_[c1] <= chunk + (chunk >> 2) && c1 - c0 < (1u << 22)) {
+            while (c1 < n && ib + lin_[c1] <= target && ob + lout_[c1] <= target + (target >> 2) &&
+                   c1 - c0 < (1u << 22)) {
                 ib += lin_[c1];
                 ob += lout_[c1];
                 mx = std::max<uint32_t>(mx, (uint32_t)std::min<uint64_t>(lin_[c1], 0xFFFFFFFFu));
                 ++c1;
             }
+            left -= ib;
             Slot& s = *slots_[k % S];
             ++k;
-            if (s.busy) finish(s, j);
+            if (s.busy) retire(s, j, tasks);  // its scatter runs in the same pass as this gather
             s.c0 = c0;
             s.c1 = c1;
             s.out_b = ob;
             s.direct_out = direct_out;
             const double t0 = now_s();
-            prepare(s, j, c0, c1, ib, ob, mx);
+            stage(s, j, c0, c1, ib, ob, tasks);
+            run_tasks(j, tasks);
             const double t1 = now_s();
+            fill(s, j, ib, ob, mx);
+            const double t2 = now_s();
             launch(s, j, ib, mx, ib != (uint64_t)(c1 - c0) * mx);
-            t_gather_ += t1 - t0;
-            t_launch_ += now_s() - t1;
+            t_copy_ += t1 - t0;
+            t_fill_ += t2 - t1;
+            t_launch_ += now_s() - t2;
             st_.chunks += 1;
             if (in_dev_) st_.direct_in += 1;
             if (direct_out) st_.direct_out += 1;
@@ -749,7 +790,12 @@ void Engine::run(const Job& j) {
         }
         for (size_t q = 0; q < S; ++q) {
             Slot& s = *slots_[(k + q) % S];
-            if (s.busy) finish(s, j);
+            if (s.busy) {
+                retire(s, j, tasks);
+                const double t0 = now_s();
+                run_tasks(j, tasks);
+                t_copy_ += now_s() - t0;
+            }
         }
     } catch (...) {
         err = std::current_exception();
@@ -757,9 +803,9 @@ void Engine::run(const Job& j) {
     if (trace_on())
         std::fprintf(stderr,
                      "[enet host] op %d mode %d n %zu in %llu out %llu chunks %zu slots %u: total %.3f ms = "
-                     "gather+small %.3f, launch %.3f, wait %.3f, scatter+small %.3f ms (direct in %d out %d)\n",
+                     "gather/scatter %.3f, small arrays %.3f, launch %.3f, wait %.3f ms (direct in %d out %d)\n",
                      (int)j.op, (int)md, n, (unsigned long long)in_total, (unsigned long long)out_total, k, S,
-                     1e3 * (now_s() - t_job), 1e3 * t_gather_, 1e3 * t_launch_, 1e3 * t_wait_, 1e3 * t_scatter_,
+                     1e3 * (now_s() - t_job), 1e3 * t_copy_, 1e3 * t_fill_, 1e3 * t_launch_, 1e3 * t_wait_,
                      in_dev_ != nullptr, (int)direct_out);
     if (err) {  // drain whatever is still in flight before the caller's buffers go away
         for (auto& s : slots_) {

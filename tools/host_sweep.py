@@ -14,18 +14,16 @@ import ephemeralnet_amd as E  # noqa: E402
 which = sys.argv[1] if len(sys.argv) > 1 else "all"
 MODES = {"zc": 0, "sdma": 1, "split": 2, "splitk": 3}
 if which in ("c2", "all"):
-    for m in ("split", "splitk", "zc"):
+    for m in os.environ.get("SWEEP_MODES", "split,splitk,zc").split(","):
         for slots in (2, 3, 4):
-            for chunk in (8, 16, 32, 64):
+            for chunk in (16, 32, 64):
                 E.set_host_mode(MODES[m])
                 r = bench.host_c2(0, 65536, 4096, 3, chunk, slots)
                 print(json.dumps({"case": "C2 e2e", "mode": m, "slots": slots, "chunk_mib": chunk,
                                   "gibs": round(r["gibs"], 2)}), flush=True)
 if which in ("c5", "all"):
-    for m, slots, chunk in [("splitk", 2, 32), ("splitk", 2, 64), ("splitk", 2, 128), ("splitk", 3, 64),
-                            ("sdma", 2, 128), ("sdma", 4, 64), ("sdma", 4, 128), ("sdma", 6, 64),
-                            ("zc", 2, 64), ("zc", 4, 64), ("zc", 4, 128), ("zc", 6, 32),
-                            ("split", 2, 128), ("split", 3, 256)]:
+    for m, slots, chunk in [("splitk", 2, 128), ("splitk", 2, 256), ("splitk", 3, 128), ("splitk", 3, 256),
+                            ("split", 3, 256), ("split", 4, 128), ("split", 2, 512)]:
         E.set_host_mode(MODES[m])
         r = bench.c5_host_timed(1, 0, 0, None, 65536, chunk, slots)
         print(json.dumps({"case": "C5 host share", "mode": m, "slots": slots, "chunk_mib": chunk,
