@@ -34,6 +34,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md chip table)
 VALU_ISSUE_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, full-rate ops only
 WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
+HOST_MODES = {0: "zero-copy kernels", 1: "SDMA per slot", 2: "SDMA split by direction",
+              3: "SDMA split by direction, kernels per slot"}
 MODE_DESC = {"aead": "AEAD seal+open", "xor": "ChaCha20 xor twice",
              "wire": "wire frames (nonce||BE32||ChaCha20(m||HMAC)) seal+open",
              "store": "chunk store (SHA-256 id + ChaCha20) + fetch (decrypt + SHA-256 check)"}
@@ -358,7 +360,7 @@ def e2e(args) -> dict:
         "open_GiBs": round(r["open_gibs"], 2),
         "pcie_bytes_per_plaintext_byte": 2.0,
         "config": {"records": args.records, "record_bytes": args.record_bytes, "chunk_mib": args.chunk_mib,
-                   "streams": args.streams, "host_buffers": "pinned", "host_mode": E.host_mode(),
+                   "streams": args.streams, "host_buffers": "pinned", "host_mode": HOST_MODES[E.host_mode()],
                    "path": "enet_pipeline_aead_seal/open (libenet_crypto.so)"},
     }
 
@@ -567,7 +569,7 @@ def c5(args) -> dict:
             "n_gpus": world,
             "config": {"workload": "C5", "records_total": r["records_total"], "bytes_total": r["bytes_total"],
                        "chunk_mib": args.c5_chunk_mib, "streams": args.c5_streams,
-                       "host_buffers": "pinned", "host_mode": E.host_mode(),
+                       "host_buffers": "pinned", "host_mode": HOST_MODES[E.host_mode()],
                        "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
     if world > 1:
@@ -980,7 +982,7 @@ def main():
                 "c5_host_is": f"BASELINE config 5 per-GPU share: {hc5['records_total']} log-uniform "
                               f"512 B-64 KiB records over {world} rank(s), AEAD + fused HMAC-SHA256 "
                               "seal+open, pinned host memory in and out, all ranks' bytes / max-over-ranks time",
-                "host_mode": "zero-copy" if E2.host_mode() == 0 else "sdma",
+                "host_mode": HOST_MODES[E2.host_mode()],
                 "path": "enet_pipeline_aead_* / enet_pipeline_aead_hmac_* (host_batch.cpp)"}
 
     if rank == 0:

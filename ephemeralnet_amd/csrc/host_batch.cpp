@@ -307,10 +307,13 @@ Mode default_mode() {
     int m = g_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char* e = std::getenv("ENET_HOST_MODE");
+        // default: copies split by direction with per-slot kernels -- measured best for uniform
+        // (C2 e2e 18.4-19.1 GiB/s) and mixed HMAC batches (C5 share 15.9) alike
+        // (profiles/r04_host_sweep_*.jsonl); zero-copy kernels reach 13-16
         m = (e && std::strcmp(e, "sdma") == 0)    ? (int)Mode::Sdma
             : (e && std::strcmp(e, "split") == 0) ? (int)Mode::SdmaSplit
-            : (e && std::strcmp(e, "splitk") == 0) ? (int)Mode::SdmaSplitK
-                                                  : (int)Mode::ZeroCopy;
+            : (e && std::strcmp(e, "zc") == 0)    ? (int)Mode::ZeroCopy
+                                                  : (int)Mode::SdmaSplitK;
         g_mode.store(m, std::memory_order_relaxed);
     }
     return (Mode)m;
@@ -700,12 +703,13 @@ void Engine::run(const Job& j) {
     const int64_t delta = delta_of(j.op);
     lin_.resize(n);
     lout_.resize(n);
-    uint64_t in_total = 0, out_total = 0;
+    uint64_t in_total = 0, out_total = 0, max_len = 0;
     for (size_t i = 0; i < n; ++i) {
         const uint64_t a = j.in_spans.empty() ? j.in_off[i + 1] - j.in_off[i] : j.in_spans[i].size();
         if (j.in_spans.empty() && j.in_off[i + 1] < j.in_off[i])
             throw std::invalid_argument("enet host batch: input offsets must be non-decreasing");
         lin_[i] = a;
+        max_len = std::max(max_len, a);
         lout_[i] = (uint64_t)std::max<int64_t>(0, (int64_t)a + delta);
         in_total += a;
         out_total += lout_[i];
@@ -732,9 +736,14 @@ void Engine::run(const Job& j) {
     }
     // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
     // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
+    // Long records behind a hash (HMAC / SHA-256 is one serial chain per record: 1.9 ms for 64 KiB)
+    // make every chunk's kernel last at least that chain, so such jobs take 8x bigger chunks
+    // (C5 share: 64 / 128 / 256 MiB chunks -> 12.2 / 14.6 / 15.9 GiB/s).
+    const bool hashes = j.op != Op::Xor && j.op != Op::AeadSeal && j.op != Op::AeadOpen;
+    const uint64_t chain = (hashes && max_len >= (16u << 10)) ? 8 : 1;
     uint64_t chunk = cfg_.chunk_bytes;
-    if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20))
-                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20));
+    if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20) * chain)
+                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20) * std::min<uint64_t>(chain, 4));
     if (!cfg_.chunk_bytes)
         if (const char* e = std::getenv("ENET_HOST_CHUNK_MIB")) chunk = std::max(1ull, std::strtoull(e, nullptr, 10)) << 20;
     st_.jobs += 1;

@@ -13,6 +13,16 @@ import ephemeralnet_amd as E  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "all"
 MODES = {"zc": 0, "sdma": 1, "split": 2, "splitk": 3}
+if which in ("c2one", "c5one"):  # one configuration from the environment (for a trace)
+    m, slots, chunk = os.environ.get("ONE", "splitk,3,256").split(",")
+    E.set_host_mode(MODES[m])
+    if which == "c2one":
+        r = bench.host_c2(0, 65536, 4096, 3, int(chunk), int(slots))
+    else:
+        r = bench.c5_host_timed(1, 0, 0, None, 65536, int(chunk), int(slots), steps=2)
+    print(json.dumps({"case": which, "mode": m, "slots": int(slots), "chunk_mib": int(chunk),
+                      "gibs": round(r["gibs"], 2)}), flush=True)
+    sys.exit(0)
 if which in ("c2", "all"):
     for m in os.environ.get("SWEEP_MODES", "split,splitk,zc").split(","):
         for slots in (2, 3, 4):
