@@ -377,7 +377,7 @@ public:
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
         slots_.clear();
-        for (hipStream_t x : {up_, down_})
+        for (hipStream_t x : {up_, kern_, down_})
             if (x) {
                 (void)hipStreamSynchronize(x);
                 (void)hipStreamDestroy(x);
@@ -407,6 +407,8 @@ private:
             if (!up_) hip_check(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking), "hipStreamCreate");
             if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
         }
+        if (mode() == Mode::SdmaSplitK && !kern_)
+            hip_check(hipStreamCreateWithFlags(&kern_, hipStreamNonBlocking), "hipStreamCreate");
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -447,6 +449,7 @@ private:
     mutable std::mutex mu_;
     std::vector<std::unique_ptr<Slot>> slots_;
     hipStream_t up_ = nullptr;    // SdmaSplit*: every H2D (and SdmaSplit: every kernel)
+    hipStream_t kern_ = nullptr;  // SdmaSplitK: every kernel
     hipStream_t down_ = nullptr;  // SdmaSplit*: every D2H
     std::unique_ptr<Pool> pool_;
     EngineStats st_{};
@@ -552,7 +555,7 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     const Layout& l = s.lay;
     const uint32_t m = (uint32_t)(s.c1 - s.c0);
     // SdmaSplit: H2D + kernel of every chunk on the up stream, D2H on the down stream;
-    // SdmaSplitK: H2D on up, kernel on the slot's stream, D2H on down
+    // SdmaSplitK: H2D on up, kernels on kern, D2H on down
     hipStream_t st = split_dirs(md) ? up_ : s.stream;
     // device addresses of this chunk's arenas and small block
     const uint8_t* din;
@@ -565,7 +568,7 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
         if (md == Mode::SdmaSplitK) {
             hip_check(hipEventRecord(s.indone, st), "hipEventRecord");
-            st = s.stream;
+            st = kern_;
             hip_check(hipStreamWaitEvent(st, s.indone, 0), "hipStreamWaitEvent");
         }
         din = s.d_in.p;
@@ -821,7 +824,7 @@ void Engine::run(const Job& j) {
             if (s->stream) (void)hipStreamSynchronize(s->stream);
             s->busy = false;
         }
-        for (hipStream_t x : {up_, down_})
+        for (hipStream_t x : {up_, kern_, down_})
             if (x) (void)hipStreamSynchronize(x);
         std::rethrow_exception(err);
     }

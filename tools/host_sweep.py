@@ -25,15 +25,15 @@ if which in ("c2one", "c5one"):  # one configuration from the environment (for a
     sys.exit(0)
 if which in ("c2", "all"):
     for m in os.environ.get("SWEEP_MODES", "split,splitk,zc").split(","):
-        for slots in (2, 3, 4):
+        for slots in (3, 4):
             for chunk in (16, 32, 64):
                 E.set_host_mode(MODES[m])
                 r = bench.host_c2(0, 65536, 4096, 3, chunk, slots)
                 print(json.dumps({"case": "C2 e2e", "mode": m, "slots": slots, "chunk_mib": chunk,
                                   "gibs": round(r["gibs"], 2)}), flush=True)
 if which in ("c5", "all"):
-    for m, slots, chunk in [("splitk", 2, 128), ("splitk", 2, 256), ("splitk", 3, 128), ("splitk", 3, 256),
-                            ("split", 3, 256), ("split", 4, 128), ("split", 2, 512)]:
+    for m, slots, chunk in [("splitk", 3, 128), ("splitk", 3, 256), ("splitk", 4, 128), ("splitk", 4, 256),
+                            ("splitk", 3, 512), ("splitk", 6, 64), ("splitk", 6, 128)]:
         E.set_host_mode(MODES[m])
         r = bench.c5_host_timed(1, 0, 0, None, 65536, chunk, slots)
         print(json.dumps({"case": "C5 host share", "mode": m, "slots": slots, "chunk_mib": chunk,
