@@ -355,6 +355,7 @@ struct Slot {
     DevBuf d_in, d_out, d_small;
     // the chunk in flight
     bool busy = false;
+    uint64_t seq = 0;  // chunk number within the job
     size_t c0 = 0, c1 = 0;
     uint64_t out_b = 0;
     bool direct_out = false;
@@ -377,7 +378,7 @@ public:
             if (s.stream) (void)hipStreamDestroy(s.stream);
         }
         slots_.clear();
-        for (hipStream_t x : {up_, kern_, down_})
+        for (hipStream_t x : {up_, kern_[0], kern_[1], down_})
             if (x) {
                 (void)hipStreamSynchronize(x);
                 (void)hipStreamDestroy(x);
@@ -407,8 +408,9 @@ private:
             if (!up_) hip_check(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking), "hipStreamCreate");
             if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
         }
-        if (mode() == Mode::SdmaSplitK && !kern_)
-            hip_check(hipStreamCreateWithFlags(&kern_, hipStreamNonBlocking), "hipStreamCreate");
+        if (mode() == Mode::SdmaSplitK)
+            for (hipStream_t& k : kern_)
+                if (!k) hip_check(hipStreamCreateWithFlags(&k, hipStreamNonBlocking), "hipStreamCreate");
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -449,7 +451,7 @@ private:
     mutable std::mutex mu_;
     std::vector<std::unique_ptr<Slot>> slots_;
     hipStream_t up_ = nullptr;    // SdmaSplit*: every H2D (and SdmaSplit: every kernel)
-    hipStream_t kern_ = nullptr;  // SdmaSplitK: every kernel
+    hipStream_t kern_[2] = {};    // SdmaSplitK: the kernels, alternating by chunk
     hipStream_t down_ = nullptr;  // SdmaSplit*: every D2H
     std::unique_ptr<Pool> pool_;
     EngineStats st_{};
@@ -568,7 +570,7 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
         if (md == Mode::SdmaSplitK) {
             hip_check(hipEventRecord(s.indone, st), "hipEventRecord");
-            st = kern_;
+            st = kern_[s.seq & 1];  // two kernel streams: consecutive chunks' hash chains overlap
             hip_check(hipStreamWaitEvent(st, s.indone, 0), "hipStreamWaitEvent");
         }
         din = s.d_in.p;
@@ -764,9 +766,12 @@ void Engine::run(const Job& j) {
             // ramped chunk sizes: the first chunks (nothing to overlap their copy in yet) and
             // the last ones (nothing left to overlap their copy out) are small, 1/8 .. 1/2 of the
             // steady chunk, so the pipeline fills and drains in a fraction of a chunk's time
+            // (not at the end when the chunk's kernel is a long hash chain: each extra chunk
+            // costs one more ~2 ms chain after the copies are done)
             uint64_t target = chunk;
             if (k < 3) target = std::max<uint64_t>(chunk >> (3 - k), 1);
-            if (left < 2 * chunk) target = std::min<uint64_t>(target, std::max<uint64_t>(left / 2, chunk >> 3));
+            if (left < 2 * chunk && chain == 1)
+                target = std::min<uint64_t>(target, std::max<uint64_t>(left / 2, chunk >> 3));
             size_t c1 = c0 + 1;
             uint64_t ib = lin_[c0], ob = lout_[c0];
             uint32_t mx = (uint32_t)std::min<uint64_t>(lin_[c0], 0xFFFFFFFFu);
@@ -783,6 +788,7 @@ void Engine::run(const Job& j) {
             if (s.busy) retire(s, j, tasks);  // its scatter runs in the same pass as this gather
             s.c0 = c0;
             s.c1 = c1;
+            s.seq = k - 1;
             s.out_b = ob;
             s.direct_out = direct_out;
             const double t0 = now_s();
@@ -824,7 +830,7 @@ void Engine::run(const Job& j) {
             if (s->stream) (void)hipStreamSynchronize(s->stream);
             s->busy = false;
         }
-        for (hipStream_t x : {up_, kern_, down_})
+        for (hipStream_t x : {up_, kern_[0], kern_[1], down_})
             if (x) (void)hipStreamSynchronize(x);
         std::rethrow_exception(err);
     }

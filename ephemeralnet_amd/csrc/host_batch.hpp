@@ -78,10 +78,10 @@ struct Job {
 //   SdmaSplit-- the same copies, but every H2D and kernel on one "up" stream and every D2H on
 //               one "down" stream (an event per slot hands the chunk over), so each copy engine
 //               direction sees back-to-back copies
-//   SdmaSplitK -- three streams: H2D on "up", kernels on "kern", D2H on "down", events between
-//               them, so neither copy direction ever waits behind a kernel (mixed batches whose
-//               serial HMAC chains last ~2 ms per launch) and no two streams share one of the
-//               box's four hardware queues
+//   SdmaSplitK -- four streams: H2D on "up", kernels alternating over two kernel streams, D2H
+//               on "down", events between them, so neither copy direction ever waits behind a
+//               kernel, consecutive chunks' hash chains (~2 ms per launch for 64 KiB records)
+//               overlap, and no two streams share one of the box's four hardware queues
 enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2, SdmaSplitK = 3 };
 
 struct Config {

@@ -509,8 +509,12 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         const uint32_t dme = (ib + (wgid0 + lane) * Lu) & 127u;
         // 32-bit line offsets from the 128-byte-aligned bases (the host launches this variant only
         // for arenas < 4 GiB)
-        const uint8_t* ial = ibase - (ib & 127u);
-        uint8_t* oal = obase - (ib & 127u);
+        // the line bases are workgroup-uniform: pin them in SGPRs (the compiler kept them in
+        // VGPRs and re-read them with two v_readfirstlane + s_nop 4 before every line load / store)
+        const uint8_t* ial = reinterpret_cast<const uint8_t*>(
+            __builtin_amdgcn_readfirstlane((uint64_t)reinterpret_cast<uintptr_t>(ibase - (ib & 127u))));
+        uint8_t* oal = reinterpret_cast<uint8_t*>(
+            __builtin_amdgcn_readfirstlane((uint64_t)reinterpret_cast<uintptr_t>(obase - (ib & 127u))));
         uint32_t roff[8];  // line 0 of owner o
         uint32_t rgeo[8];  // d | lines << 8 | end-bytes-in-last-line << 16
 #pragma unroll
@@ -525,6 +529,14 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         }
         uint32_t pf[32];
         auto fetch = [&](uint32_t t) {  // line t of every role owner -> pf (only lines it has)
+            if (t < S) {  // every record has lines 0 .. S-1 (S = ceil(L / 128) <= its line count)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ial + (roff[i] + 128u * t + 16u * rc));
+                    pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 if (t < ((rgeo[i] >> 8) & 0xffu)) {

@@ -248,8 +248,8 @@ ENET_API int enet_pipeline_wire_open(enet_pipeline* pipe, const enet_records* ho
 /* How host-resident batches reach the kernels (pipelines and crypto::batch::*), process-wide:
  * 0 = zero-copy -- the kernels read and write pinned host memory directly over PCIe;
  * 1 = SDMA -- H2D copy, kernel, D2H copy per chunk on the chunk's stream; 2 = SDMA
- * with every H2D + kernel on one stream and every D2H on another; 3 = SDMA with H2D, kernels
- * and D2H on three streams of their own (the default).
+ * with every H2D + kernel on one stream and every D2H on another; 3 = SDMA with H2D on one
+ * stream, kernels alternating over two more and D2H on a fourth (the default).
  * ENET_HOST_MODE=zc|sdma|split|splitk sets the initial value.  Results are identical. */
 ENET_API int enet_host_set_mode(int mode);
 ENET_API int enet_host_mode(void);
