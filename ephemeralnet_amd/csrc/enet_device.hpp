@@ -581,6 +581,14 @@ __device__ __forceinline__ void store_block(uint8_t* __restrict__ p, uint32_t n,
     }
 }
 
+// A workgroup-uniform 64-bit value (a base address) pinned in an SGPR pair.  readfirstlane is a
+// 32-bit operation returning int: read both halves and zero-extend the low one (passing the
+// 64-bit value to the builtin truncates it to 32 bits -- an illegal address).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }

@@ -511,10 +511,9 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
         // for arenas < 4 GiB)
         // the line bases are workgroup-uniform: pin them in SGPRs (the compiler kept them in
         // VGPRs and re-read them with two v_readfirstlane + s_nop 4 before every line load / store)
-        const uint8_t* ial = reinterpret_cast<const uint8_t*>(
-            __builtin_amdgcn_readfirstlane((uint64_t)reinterpret_cast<uintptr_t>(ibase - (ib & 127u))));
-        uint8_t* oal = reinterpret_cast<uint8_t*>(
-            __builtin_amdgcn_readfirstlane((uint64_t)reinterpret_cast<uintptr_t>(obase - (ib & 127u))));
+        const uint8_t* ial =
+            reinterpret_cast<const uint8_t*>(uniform_u64(reinterpret_cast<uintptr_t>(ibase - (ib & 127u))));
+        uint8_t* oal = reinterpret_cast<uint8_t*>(uniform_u64(reinterpret_cast<uintptr_t>(obase - (ib & 127u))));
         uint32_t roff[8];  // line 0 of owner o
         uint32_t rgeo[8];  // d | lines << 8 | end-bytes-in-last-line << 16
 #pragma unroll
