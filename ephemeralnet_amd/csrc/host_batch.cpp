@@ -702,7 +702,7 @@ void Engine::run(const Job& j) {
         const char* e = std::getenv("ENET_HOST_SLOTS");
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
     }();
-    const uint32_t S = std::min<uint32_t>(cfg_.slots ? cfg_.slots : env_slots ? env_slots : 3u, 8);
+    const uint32_t S = std::min<uint32_t>(cfg_.slots ? cfg_.slots : env_slots ? env_slots : 4u, 8);
     setup_slots(S);
     // lengths
     const int64_t delta = delta_of(j.op);
@@ -742,10 +742,11 @@ void Engine::run(const Job& j) {
     // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
     // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
     // Long records behind a hash (HMAC / SHA-256 is one serial chain per record: 1.9 ms for 64 KiB)
-    // make every chunk's kernel last at least that chain, so such jobs take 8x bigger chunks
-    // (C5 share: 64 / 128 / 256 MiB chunks -> 12.2 / 14.6 / 15.9 GiB/s).
+    // make every chunk's kernel last at least that chain, so such jobs take 4x bigger chunks
+    // (C5 share, 4 slots, two kernel streams: 128 / 256 MiB chunks -> 18.6 / 17.4 GiB/s,
+    // profiles/r04_host_sweep_p7b.jsonl; one kernel stream peaked at 256 MiB).
     const bool hashes = j.op != Op::Xor && j.op != Op::AeadSeal && j.op != Op::AeadOpen;
-    const uint64_t chain = (hashes && max_len >= (16u << 10)) ? 8 : 1;
+    const uint64_t chain = (hashes && max_len >= (16u << 10)) ? 4 : 1;
     uint64_t chunk = cfg_.chunk_bytes;
     if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20) * chain)
                                                 : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20) * std::min<uint64_t>(chain, 4));
