@@ -31,26 +31,12 @@
 // (the caller's hints declared the batch uniform); if any does not, the whole workgroup runs the
 // per-lane path of records_body.hpp instead (COOP 7), so a wrong hint costs speed, never bytes.
 //
-// TAIL variant (one lane per record, L a multiple of 4 but not of 128, L >= 128: C3's 1 500-byte
-// relay frames): the same kernel over records that do not start on lines.  Stage st of record g
-// is its bytes [128 st, 128 st + 128) at arena offset g L + 128 st -- the same run layout in LDS,
-// so the keystream waves are unchanged; the memory waves' 16-byte loads and stores are merely
-// 4-byte aligned and each run touches two lines, whose halves meet in L2 one stage apart (plain
-// loads and stores instead of non-temporal ones, so the line stays for its second half).  The
-// last stage is partial: its DMA reads up to 128 - L mod 128 bytes of the NEXT record (the host
-// leaves at least one record after the launch and every workgroup checks that record is long
-// enough), its keystream is computed whole, Poly1305 takes only the ceil(L/16) - 8 (S-1)
-// remaining blocks (zero-padded, RFC 8439 2.8), and its stores are dword-exact.
-//
 // Reference behaviour: ChaCha20::apply (src/crypto/ChaCha20.cpp:98-121, u32 counter wrap :110)
 // for MODE_XOR; RFC 8439 AEAD (no reference implementation) for seal / open.
-#include "records_body.hpp"
+#include "stream_common.hpp"
 
 namespace enet {
 
-constexpr uint32_t kStreamLanes = 512;    // record lanes per workgroup (8 compute waves)
-constexpr uint32_t kStreamWG = 768;       // + 4 memory waves
-constexpr int kStreamSteps = 76;          // keystream barriers per stage (19 lockstep half-rounds)
 // Memory-wave schedule, in keystream barrier positions (an op at position k runs between barriers
 // k-1 and k; a step is ~276 shader cycles of compute, a 1 KiB DMA or store costs its memory
 // wave ~100-140 cycles to issue, so no position carries more than one of them -- two pushed
@@ -80,26 +66,8 @@ __device__ constexpr int stream_stores_after(StreamSched sc) {
     return n;
 }
 
-__device__ __forceinline__ void stream_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
-// Poly1305 over the first nb16 16-byte blocks of a 128-byte run (the last stage of a TAIL record,
-// bytes >= rem zeroed first; rem is a multiple of 4, uniform across the workgroup)
-__device__ __forceinline__ void poly_run_tail(uint32_t h[5], const PolyR32& R, const uint32_t w[32], uint32_t rem) {
-    const uint32_t nb16 = (rem + 15u) >> 4;
-#pragma unroll
-    for (uint32_t u = 0; u < 8; ++u) {
-        if (u < nb16) {
-            uint32_t m[4];
-#pragma unroll
-            for (uint32_t i = 0; i < 4; ++i) m[i] = (4u * (4u * u + i) < rem) ? w[4 * u + i] : 0u;
-            poly32_block(h, R, m[0], m[1], m[2], m[3], 1u);
-        }
-    }
-}
-
-template <int LOGP, int MODE, int SCHED = 0, bool TAIL = false>
+template <int LOGP, int MODE, int SCHED = 0>
 __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
-    static_assert(!TAIL || LOGP == 0, "the TAIL variant runs one lane per record");
     constexpr StreamSched SC = stream_sched(SCHED);
     constexpr int BARF = stream_barf(SCHED);       // keystream steps per barrier
     constexpr int kPos = kStreamSteps / BARF;      // barrier positions per stage
@@ -132,21 +100,11 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         stamps[1] = __builtin_amdgcn_s_memtime();
     }
     const uint64_t i0 = p.in_off[0], o0 = p.out_off[0];
-    // blocks per lane (the host launches L % (128 P) == 0, or TAIL) and stages
-    const uint32_t B = TAIL ? (L + 63u) >> 6 : L >> (6 + LOGP);
-    const uint32_t S = (B + 1u) >> 1;
     {
-        bool mine = !compute || (p.in_off[rec] == i0 + (uint64_t)rec * L &&
-                                 p.in_off[rec + 1] == i0 + (uint64_t)(rec + 1) * L &&
-                                 p.out_off[rec] == o0 + (uint64_t)rec * L &&
-                                 p.out_off[rec + 1] == o0 + (uint64_t)(rec + 1) * L);
-        // TAIL: the last stage's DMA over-reads 128 S - L bytes past the record: the next record
-        // (the launch never holds the batch's last one) must be at least that long, and the
-        // dword-exact stores need 4-byte-aligned record starts
-        if (TAIL && compute)
-            mine = mine && p.in_off[rec + 2] >= i0 + (uint64_t)(rec + 1) * L + (128ull * S - L) &&
-                   ((reinterpret_cast<uintptr_t>(p.in) + i0) & 3u) == 0 &&
-                   ((reinterpret_cast<uintptr_t>(p.out) + o0) & 3u) == 0;
+        const bool mine = !compute || (p.in_off[rec] == i0 + (uint64_t)rec * L &&
+                                       p.in_off[rec + 1] == i0 + (uint64_t)(rec + 1) * L &&
+                                       p.out_off[rec] == o0 + (uint64_t)rec * L &&
+                                       p.out_off[rec + 1] == o0 + (uint64_t)(rec + 1) * L);
         if (!__syncthreads_and(mine ? 1 : 0)) {
             if (compute) records_body<LOGP, MODE, FR_NONE, 7>(p);
             return;
@@ -155,6 +113,8 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t B = L >> (6 + LOGP);  // blocks per lane (the host launches L % (128 P) == 0)
+    const uint32_t S = B >> 1;           // stages
     const bool mem = !(dbg & 1);
 
     if (!compute) {
@@ -216,7 +176,7 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             uint32_t keep;
             // non-temporal: every input line is read exactly once (C2: +1.2 %, three interleaved
             // pairs, tools/stagger_ab.sh "0 14"; SCHED 14 = plain loads for the A/B)
-            if constexpr (SCHED == 14 || TAIL)
+            if constexpr (SCHED == 14)
                 asm volatile("s_mov_b32 %0, m0\n s_mov_b32 m0, %2\n s_nop 0\n global_load_lds_dwordx4 %1, %3\n s_mov_b32 m0, %0"
                              : "=&s"(keep) : "v"(offs[s]), "s"(m0), "s"(base) : "memory");
             else
@@ -231,12 +191,8 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         // store is absent from the compiler's vmcnt bookkeeping: the stage-end waits count it.
         auto store = [&](uint8_t* base, int s, uint4 v) {
             enet_u32x4 d = {v.x, v.y, v.z, v.w};
-            if constexpr (TAIL)  // half lines: L2 merges them with the next stage's halves
-                asm volatile("global_store_dwordx4 %0, %1, %2\n s_nop 1"
-                             :: "v"(offs[s]), "v"(d), "s"(base) : "memory");
-            else
-                asm volatile("global_store_dwordx4 %0, %1, %2 nt\n s_nop 1"
-                             :: "v"(offs[s]), "v"(d), "s"(base) : "memory");
+            asm volatile("global_store_dwordx4 %0, %1, %2 nt\n s_nop 1"
+                         :: "v"(offs[s]), "v"(d), "s"(base) : "memory");
         };
         uint64_t wait_cyc = 0;
         if (mem) {
@@ -280,29 +236,8 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
         stream_barrier();  // F1: the last stage's outputs are in slab (S-1) & 1
         if (S > 0 && mem) {
             uint8_t* olast = obase + (size_t)kRun * (S - 1);
-            if constexpr (TAIL) {
-                // the partial stage: chunk c of the run holds record bytes [16 c, 16 c + 16) of
-                // the rem = L - 128 (S-1) left; only those are stored, dword-exact
-                const uint32_t rem = L - kRun * (S - 1);
-                const uint32_t cs[2] = {kk ^ slab_sw(lane >> 3), kk ^ slab_sw(8u + (lane >> 3))};
 #pragma unroll
-                for (int s = 0; s < 16; ++s) {
-                    const uint4 v = ldsread(s);
-                    const uint32_t c0 = 16u * cs[s & 1];
-                    uint8_t* q = olast + offs[s];
-                    if (c0 + 16u <= rem) {
-                        *reinterpret_cast<uint4*>(q) = v;
-                    } else if (c0 < rem) {
-                        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (uint32_t m = 0; m < 3; ++m)
-                            if (c0 + 4u * m < rem) reinterpret_cast<uint32_t*>(q)[m] = w4[m];
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < 16; ++s) store(olast, s, ldsread(s));
-            }
+            for (int s = 0; s < 16; ++s) store(olast, s, ldsread(s));
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store done (tamper zeroing)
         stream_barrier();  // F2
@@ -421,16 +356,9 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
                 chacha_half_lockstep2<true, NoStepHook, BARF>(x);
             }
         }
-        // TAIL: the last stage holds rem = L - 128 (S-1) record bytes (uniform)
-        const bool part = TAIL && st + 1 == S;
-        const uint32_t rem = L - kRun * st;
         if (MODE == MODE_OPEN && !(dbg & 4)) {
-            if (part) {
-                poly_run_tail(h, PR, w, rem);
-            } else {
-                poly_block64(h, PR, w);
-                poly_block64(h, PR, w + 16);
-            }
+            poly_block64(h, PR, w);
+            poly_block64(h, PR, w + 16);
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -438,12 +366,8 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
             w[16 + i] ^= x[16 + i] + (i == 12 ? c0 + 1u : ff[i]);
         }
         if (MODE == MODE_SEAL && !(dbg & 4)) {
-            if (part) {
-                poly_run_tail(h, PR, w, rem);
-            } else {
-                poly_block64(h, PR, w);
-                poly_block64(h, PR, w + 16);
-            }
+            poly_block64(h, PR, w);
+            poly_block64(h, PR, w + 16);
         }
         // outputs into the own run of the output slab (the memory waves have read its previous
         // contents out by now)
@@ -517,22 +441,13 @@ __global__ __launch_bounds__(kStreamWG) void stream_kernel(RecParams p) {
     if (MODE == MODE_OPEN && diff != 0) {
         // authentication failed: do not release plaintext
         uint8_t* seg = p.out + o0 + (uint64_t)rec * L + ((uint64_t)j * B << 6);
-        if (TAIL) {  // exactly the record's L bytes (4-byte aligned)
-            for (uint32_t c = 0; c < (L >> 2); ++c) reinterpret_cast<uint32_t*>(seg)[c] = 0u;
-        } else {
-            for (uint32_t c = 0; c < 4 * B; ++c)
-                *reinterpret_cast<uint4*>(seg + 16ull * c) = make_uint4(0, 0, 0, 0);
-        }
+        for (uint32_t c = 0; c < 4 * B; ++c)
+            *reinterpret_cast<uint4*>(seg + 16ull * c) = make_uint4(0, 0, 0, 0);
     }
 }
 
 template <int MODE>
 static hipError_t launch_stream_mode(const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s) {
-    if (p.uniform_len % 128u != 0) {  // TAIL (stream_tail_eligible)
-        if (lanes != 1) return hipErrorInvalidValue;
-        hipLaunchKernelGGL((stream_kernel<0, MODE, 0, true>), dim3(blocks), dim3(kStreamWG), 0, s, p);
-        return hipGetLastError();
-    }
     switch (lanes) {
         case 1: hipLaunchKernelGGL((stream_kernel<0, MODE>), dim3(blocks), dim3(kStreamWG), 0, s, p); break;
         case 2:
@@ -563,15 +478,6 @@ bool stream_eligible(const RecParams& p, uint32_t lanes) {
     const uint64_t L = p.uniform_len;
     return (p.stream & 1) && L != 0 && p.order == nullptr && L % (128ull * lanes) == 0 &&
            L * (uint64_t)p.n <= 0xFFFFFFFFull && p.n >= kStreamLanes / lanes;
-}
-
-// TAIL: one lane per record, L % 4 == 0, L >= 128 (the over-read of the last stage stays inside
-// the next record), and at least one record after the launched ones (n > 512: the launch covers
-// (n - 1) / 512 whole workgroups)
-bool stream_tail_eligible(const RecParams& p, uint32_t lanes) {
-    const uint64_t L = p.uniform_len;
-    return (p.stream & 2) && lanes == 1 && L >= 128 && L % 128 != 0 && L % 4 == 0 && p.order == nullptr &&
-           L * (uint64_t)p.n <= 0xFFFFFFFFull - 256 && p.n > kStreamLanes;
 }
 
 hipError_t launch_stream(int mode, const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s) {

@@ -1,9 +1,9 @@
 #!/bin/bash
-# round-4: the stream kernel's TAIL variant for C3 (parity first), C3 A/B against line staging,
+# round-4: the stream kernel's stream tail kernel for C3 (parity first), C3 A/B against line staging,
 # C3 PMC, and the default bench line beside one-shot host pipeline runs on the same box.
-# usage (on the box): bash tools/gpu_p8.sh TAG
+# usage (on the box): bash tools/gpu_p9.sh TAG
 set -o pipefail
-T=${1:-p8}
+T=${1:-p9}
 O=gpurun_out/$T
 mkdir -p $O
 export TMPDIR=/tmp
