@@ -30,4 +30,11 @@ for one in c2one:splitk,4,32 c5one:splitk,4,128 c2one:splitk,3,32; do
   ONE=${one#*:} timeout -k 10 200 python -u tools/host_sweep.py ${one%%:*} >> $O/sweep.jsonl 2>> $O/sweep.err || { echo sweep failed; exit 1; }
 done
 cat $O/sweep.jsonl
+step e2e variants
+for a in "" "--chunk-mib 32 --streams 4" "--chunk-mib 32" "--streams 4"; do
+  timeout -k 10 120 python bench.py --e2e $a > $O/x.json 2>> $O/e2e.err || { echo e2e failed; exit 1; }
+  python -c "import json; d=json.load(open('$O/x.json')); print('e2e [$a]', d['value'], d['seal_GiBs'], d['open_GiBs'])" | tee -a $O/e2e.txt
+done
+ENET_HOST_TRACE=1 timeout -k 10 120 python bench.py --e2e > $O/x.json 2> $O/e2e_trace.err || { echo e2e failed; exit 1; }
+tail -5 $O/e2e_trace.err
 step done
