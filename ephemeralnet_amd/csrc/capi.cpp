@@ -88,12 +88,9 @@ enet::RecParams rec_params(const enet_records* r) {
         return (e && e[0] == '1') ? 1 : 0;
     }();
     if (dflt && lines_lock) p.coop_lines = 2;
-    // ENET_STREAM: bit 0 = the streaming kernel for line-multiple records (stream.hip), bit 1 =
-    // the streaming tail kernel for unaligned one-lane records (stream_tail.hip); default 3
-    // (1 = line staging for the latter instead)
     static const int strm = [] {
         const char* e = std::getenv("ENET_STREAM");
-        return e ? (int)(std::strtol(e, nullptr, 10) & 3) : 3;
+        return (e && e[0] == '0') ? 0 : 1;
     }();
     p.stream = dflt ? strm : 0;
 #ifdef ENET_TOOLS_BUILD

@@ -59,8 +59,6 @@ struct RecParams {
 hipError_t launch_records(int mode, const RecParams& p, uint32_t lanes, hipStream_t s);
 // The streaming kernel (stream.hip): whole 512-thread workgroups of a uniform batch.
 bool stream_eligible(const RecParams& p, uint32_t lanes);
-bool stream_tail_eligible(const RecParams& p, uint32_t lanes);
-hipError_t launch_stream_tail(int mode, const RecParams& p, uint32_t blocks, hipStream_t s);
 hipError_t launch_stream(int mode, const RecParams& p, uint32_t lanes, uint32_t blocks, hipStream_t s);
 
 struct ShaParams {

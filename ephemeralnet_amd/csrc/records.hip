@@ -46,20 +46,6 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
         }
         return hipGetLastError();
     }
-    if (FRAME == FR_NONE && LOGP == 0 && stream_tail_eligible(p, 1u)) {
-        // unaligned one-lane records (C3): the streaming tail kernel (stream_tail.hip) over whole
-        // workgroups, keeping at least one record after them (its last stage over-reads into
-        // the next record); the rest (1 .. 512 records) per lane
-        const uint32_t full = (p.n - 1u) / 512u;
-        RecParams q = p;
-        q.n = full * 512u;
-        if (hipError_t e = launch_stream_tail(MODE, q, full, s)) return e;
-        RecParams r = p;
-        r.n = p.n - q.n;
-        r.rec_base = q.n;
-        hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 0>), dim3((r.n + kWG - 1) / kWG), dim3(kWG), 0, s, r);
-        return hipGetLastError();
-    }
     if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop >= 1) {
         // Cooperative kernels over whole workgroups of records (no dead owners, no store
         // predicates); the remaining records go through the per-lane kernel.

@@ -1,5 +1,4 @@
-// stream_common.hpp -- shape constants shared by the streaming kernels (stream.hip: records that
-// are whole lines; stream_tail.hip: one-lane records that are not).
+// stream_common.hpp -- shape constants of the streaming kernel (stream.hip).
 #pragma once
 #include "records_body.hpp"
 

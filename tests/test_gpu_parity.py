@@ -823,11 +823,10 @@ def test_stream_kernel_unaligned_arenas(enet, ishift, oshift):
 @pytest.mark.parametrize("L", [1500, 1436, 1284, 260, 132, 196, 4100, 1504, 1496, 136, 4092])
 @pytest.mark.parametrize("ishift,oshift", [(0, 0), (4, 4), (8, 100), (0, 12), (64, 0), (2, 0), (0, 1)])
 def test_uniform_one_lane_shapes(enet, L, ishift, oshift):
-    """Uniform one-lane batches whose length is not a multiple of 128 (C3 class: the streaming tail
-    kernel over whole 512-record workgroups, keeping one record after them, the rest per lane):
-    record starts at every 4-byte phase of a 16-byte window and of a line (L mod 16 = 12, 4, 0, 8),
-    two to 32 stages, tails of 4 to 124 bytes, arenas off alignment (in / out phases that differ
-    take separate windows; a 2- or 1-byte shift takes the per-lane path).  Seal bit-exact against the oracle
+    """Uniform one-lane batches whose length is not a multiple of 128 (C3 class: line staging over
+    whole workgroups, the rest per lane): record starts at every 4-byte phase of a line (L mod 16 =
+    12, 4, 0, 8), two to 33 stages, tails of 4 to 124 bytes, arenas off alignment (in / out phases
+    that differ, or a 2- or 1-byte shift, take the per-lane path).  Seal bit-exact against the oracle
     at every record of the first workgroup's edges and a sample, nothing written outside the
     output arena, open(seal(x)) == x, a tampered record (first, middle and last unit) rejected
     and zeroed with its neighbours intact, and reference-mode ChaCha20 with counters at the
