@@ -14,4 +14,6 @@ for o in torch_first lib_first torch_first lib_first; do
   timeout -k 10 120 python tools/e2e_probe.py $o >> $O/e2e_probe.jsonl 2>> $O/e2e_probe.err || { echo probe failed; exit 1; }
   tail -1 $O/e2e_probe.jsonl
 done
+step c2 copy trace
+ONE=splitk,4,32 timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace -o c2 -- python3 tools/host_sweep.py c2one > $O/c2trace.json 2> $O/c2trace.err; rc=$?; cat $O/c2trace.json; [ $rc -eq 0 ] || exit $rc
 step done
