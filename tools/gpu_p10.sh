@@ -16,4 +16,5 @@ for o in torch_first lib_first torch_first lib_first; do
 done
 step c2 copy trace
 ONE=splitk,4,32 timeout -k 10 180 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace -o c2 -- python3 tools/host_sweep.py c2one > $O/c2trace.json 2> $O/c2trace.err; rc=$?; cat $O/c2trace.json; [ $rc -eq 0 ] || exit $rc
+python tools/copy_trace.py $O/trace/c2 > $O/c2trace_summary.jsonl; cat $O/c2trace_summary.jsonl
 step done
