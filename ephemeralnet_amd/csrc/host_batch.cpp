@@ -395,22 +395,36 @@ public:
 
 private:
     Mode mode() const { return cfg_.mode >= 0 ? (Mode)cfg_.mode : default_mode(); }
-    void setup_slots(uint32_t S) {
+    // Streams are created only when a job needs them: the box maps every stream of the process
+    // (torch's included, when the library runs on torch's HIP runtime) onto GPU_MAX_HW_QUEUES = 4
+    // hardware queues, and streams that share a queue serialise.  Eight streams (4 slot streams
+    // that split modes never use + up, 2 kernel, down) put the H2D and D2H streams behind each
+    // other: C2 e2e 12.4 GiB/s in bench.py (torch's runtime) against 18.5 with the library's own
+    // runtime, same box (profiles/r04_e2e_variants_bench_process.txt, r04d_host_oneshots.jsonl).
+    // Split modes: up + down (+ one kernel stream, + a second one for hash-chain-bound jobs).
+    void setup_slots(uint32_t S, bool chain) {
+        const Mode md = mode();
+        auto make = [](hipStream_t& x) {
+            if (!x) hip_check(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate");
+        };
         while (slots_.size() < S) {
             slots_.emplace_back(std::make_unique<Slot>());
             Slot& s = *slots_.back();
-            hip_check(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
             hip_check(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
             hip_check(hipEventCreateWithFlags(&s.kdone, hipEventDisableTiming), "hipEventCreate");
             hip_check(hipEventCreateWithFlags(&s.indone, hipEventDisableTiming), "hipEventCreate");
         }
-        if (split_dirs(mode())) {
-            if (!up_) hip_check(hipStreamCreateWithFlags(&up_, hipStreamNonBlocking), "hipStreamCreate");
-            if (!down_) hip_check(hipStreamCreateWithFlags(&down_, hipStreamNonBlocking), "hipStreamCreate");
+        if (!split_dirs(md)) {
+            for (uint32_t i = 0; i < S; ++i) make(slots_[i]->stream);
+            return;
         }
-        if (mode() == Mode::SdmaSplitK)
-            for (hipStream_t& k : kern_)
-                if (!k) hip_check(hipStreamCreateWithFlags(&k, hipStreamNonBlocking), "hipStreamCreate");
+        make(up_);
+        make(down_);
+        if (md == Mode::SdmaSplitK) {
+            make(kern_[0]);
+            if (chain) make(kern_[1]);
+        }
+        nkern_ = (md == Mode::SdmaSplitK && chain) ? 2u : 1u;
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -451,7 +465,8 @@ private:
     mutable std::mutex mu_;
     std::vector<std::unique_ptr<Slot>> slots_;
     hipStream_t up_ = nullptr;    // SdmaSplit*: every H2D (and SdmaSplit: every kernel)
-    hipStream_t kern_[2] = {};    // SdmaSplitK: the kernels, alternating by chunk
+    hipStream_t kern_[2] = {};    // SdmaSplitK: the kernels (alternating by chunk for chain-bound jobs)
+    uint32_t nkern_ = 1;          // kernel streams of the current job
     hipStream_t down_ = nullptr;  // SdmaSplit*: every D2H
     std::unique_ptr<Pool> pool_;
     EngineStats st_{};
@@ -570,7 +585,8 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
         if (md == Mode::SdmaSplitK) {
             hip_check(hipEventRecord(s.indone, st), "hipEventRecord");
-            st = kern_[s.seq & 1];  // two kernel streams: consecutive chunks' hash chains overlap
+            // two kernel streams for hash-chain-bound jobs: consecutive chunks' chains overlap
+            st = kern_[nkern_ > 1 ? (s.seq & 1) : 0];
             hip_check(hipStreamWaitEvent(st, s.indone, 0), "hipStreamWaitEvent");
         }
         din = s.d_in.p;
@@ -703,7 +719,6 @@ void Engine::run(const Job& j) {
         return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
     }();
     const uint32_t S = std::min<uint32_t>(cfg_.slots ? cfg_.slots : env_slots ? env_slots : 4u, 8);
-    setup_slots(S);
     // lengths
     const int64_t delta = delta_of(j.op);
     lin_.resize(n);
@@ -730,23 +745,25 @@ void Engine::run(const Job& j) {
     if (in_dev_) in_dev_ -= j.in_off[0];
     if (out_dev_) out_dev_ -= j.out_off[0];
     const bool direct_out = out_dev_ != nullptr;
+    // Long records behind a hash (HMAC / SHA-256 is one serial chain per record: 1.9 ms for 64 KiB)
+    // bound every chunk's kernel by that chain
+    const bool hashes = j.op != Op::Xor && j.op != Op::AeadSeal && j.op != Op::AeadOpen;
+    const uint64_t chain = (hashes && max_len >= (16u << 10)) ? 4 : 1;
+    setup_slots(S, chain > 1);
     // sessions: key table and its HMAC midstates on the device, once per job
     if (j.session) {
         table_.ensure(32ull * j.n_sessions);
         mid_.ensure(64ull * j.n_sessions);
-        hipStream_t s0 = slots_[0]->stream;
+        hipStream_t s0 = split_dirs(md) ? up_ : slots_[0]->stream;
         hip_check(hipMemcpyAsync(table_.p, j.keys, 32ull * j.n_sessions, hipMemcpyHostToDevice, s0), "H2D sessions");
         enet_check(enet_hmac_midstates(table_.p, j.n_sessions, reinterpret_cast<uint32_t*>(mid_.p), s0), "midstates");
         hip_check(hipStreamSynchronize(s0), "session setup");
     }
     // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
-    // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
-    // Long records behind a hash (HMAC / SHA-256 is one serial chain per record: 1.9 ms for 64 KiB)
-    // make every chunk's kernel last at least that chain, so such jobs take 4x bigger chunks
+    // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks.
+    // Chain-bound jobs take 4x bigger chunks, so every chunk's kernel lasts at least its chain
     // (C5 share, 4 slots, two kernel streams: 128 / 256 MiB chunks -> 18.6 / 17.4 GiB/s,
     // profiles/r04_host_sweep_p7b.jsonl; one kernel stream peaked at 256 MiB).
-    const bool hashes = j.op != Op::Xor && j.op != Op::AeadSeal && j.op != Op::AeadOpen;
-    const uint64_t chain = (hashes && max_len >= (16u << 10)) ? 4 : 1;
     uint64_t chunk = cfg_.chunk_bytes;
     if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20) * chain)
                                                 : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20) * std::min<uint64_t>(chain, 4));
