@@ -70,6 +70,12 @@ def parse():
                          "--chunk-mib chunks (recorded in DESIGN.md, never `value`)")
     ap.add_argument("--chunk-mib", type=int, default=0, help="host pipeline chunk size (0 = runtime default)")
     ap.add_argument("--streams", type=int, default=0, help="host pipeline slots / streams (0 = runtime default)")
+    # internal: one host-resident leg in a child process (host_child_main)
+    ap.add_argument("--host-child", choices=["c2", "c5"], default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--host-device", type=int, default=0, help=argparse.SUPPRESS)
+    for k in ("--c5-all", "--c5-lo", "--c5-hi", "--c5-rank"):
+        ap.add_argument(k, type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--c5-steps", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--no-host", action="store_true",
                     help="default line: skip the host-resident extra keys (C2 e2e, C5 per-GPU share)")
     ap.add_argument("--c5-chunk-mib", type=int, default=0,
@@ -349,8 +355,10 @@ def host_c2(dev_index: int, n: int, L: int, reps: int = 3, chunk_mib: int = 0, s
 
 
 def e2e(args) -> dict:
-    """--e2e: the C2 shape host-resident (host_c2), one line."""
+    """--e2e: the C2 shape host-resident (host_c2), one line; the library is loaded before torch
+    (the system HIP runtime, see HOST_RUNTIME)."""
     import ephemeralnet_amd as E
+    E.lib()
     r = host_c2(0, args.records, args.record_bytes, 3, args.chunk_mib, args.streams)
     return {
         "metric": "GiB/s ChaCha20-Poly1305 seal+open, host-resident (H2D + kernel + D2H)",
@@ -361,6 +369,7 @@ def e2e(args) -> dict:
         "pcie_bytes_per_plaintext_byte": 2.0,
         "config": {"records": args.records, "record_bytes": args.record_bytes, "chunk_mib": args.chunk_mib,
                    "streams": args.streams, "host_buffers": "pinned", "host_mode": HOST_MODES[E.host_mode()],
+                   "hip_runtime": "system ROCm HIP runtime (library loaded before torch)",
                    "path": "enet_pipeline_aead_seal/open (libenet_crypto.so)"},
     }
 
@@ -540,6 +549,93 @@ def c5_host_timed(world: int, rank: int, dev_index: int, red_dev, n_per_rank: in
             "bytes_total": int(lens_all.sum()), "seconds": el}
 
 
+# ---------------------------------------------------------------- host legs in a child process
+# The host pipelines are measured in a child process that loads the library BEFORE torch, so the
+# library runs on the system ROCm HIP runtime it links against -- the runtime of a C / C++ / Go
+# host calling the C ABI, the deployment INTEGRATION.md describes.  In a process that imported
+# torch first, the library resolves libamdhip64 to torch's bundled copy instead, whose SDMA copies
+# measured 12.3 vs 18.9 GiB/s for the same C2 pipeline on the same box
+# (profiles/r04_e2e_probe_hip_runtime.jsonl); that in-process figure is reported beside it.
+HOST_RUNTIME = "system ROCm HIP runtime (child process: libenet_crypto loaded before torch)"
+
+
+def host_child_main(args) -> None:
+    """--host-child c2|c5 (internal): one host-resident measurement, JSON on stdout.  c5 prints
+    "ready" after its warm-up and starts its timed steps when a line arrives on stdin, so the
+    parents can line up every rank's timed region behind a barrier."""
+    import ephemeralnet_amd as E
+    E.lib()  # before torch: the system HIP runtime
+    if args.host_child == "c2":
+        r = host_c2(args.host_device, args.records, args.record_bytes, 3, args.chunk_mib, args.streams)
+        print(json.dumps(r), flush=True)
+        return
+    lens = c5_lengths(args.c5_all)[args.c5_lo:args.c5_hi]
+    step, check, mine = host_c5_rank(args.host_device, lens, 11 + args.c5_rank, args.c5_chunk_mib,
+                                     args.c5_streams)
+    step()  # warm-up: grows the pipeline's staging
+    print("ready", flush=True)
+    sys.stdin.readline()
+    t0 = time.perf_counter()
+    for _ in range(args.c5_steps):
+        step()
+    el = time.perf_counter() - t0
+    print(json.dumps({"seconds": el, "ok": bool(check()), "bytes": int(mine)}), flush=True)
+
+
+def host_child(kind: str, dev_index: int, extra: list):
+    """Start `bench.py --host-child kind` on device dev_index (a child process: this process may
+    have initialised the GPU, so it never replaces itself by another program)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--host-child", kind, "--host-device", str(dev_index)] + extra
+    return subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+
+
+def host_c2_child(dev_index: int, n: int, L: int, chunk_mib: int, streams: int) -> dict:
+    proc = host_child("c2", dev_index, ["--records", str(n), "--record-bytes", str(L),
+                                        "--chunk-mib", str(chunk_mib), "--streams", str(streams)])
+    out, _ = proc.communicate(timeout=600)
+    if proc.returncode != 0:
+        raise SystemExit(f"host-resident C2 child failed (exit {proc.returncode})")
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def c5_host_child_timed(world: int, rank: int, dev_index: int, red_dev, n_per_rank: int, chunk_mib: int,
+                        streams: int, steps: int = 1) -> dict:
+    """c5_host_timed with each rank's share run by a child process on the system HIP runtime:
+    every child warms up, the parents barrier, then all children run their timed steps; the time
+    is the max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    from ephemeralnet_amd.shard import shard_ranges
+
+    n_all = n_per_rank * world
+    lens_all = c5_lengths(n_all)
+    lo, hi = shard_ranges(lens_all.tolist(), world)[rank]
+    proc = host_child("c5", dev_index, ["--c5-all", str(n_all), "--c5-lo", str(lo), "--c5-hi", str(hi),
+                                        "--c5-rank", str(rank), "--c5-steps", str(steps),
+                                        "--c5-chunk-mib", str(chunk_mib), "--c5-streams", str(streams)])
+    ready = proc.stdout.readline().strip() == "ready"
+    if world > 1:
+        flag = torch.tensor([0.0 if ready else 1.0], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        ready = ready and flag.item() == 0.0
+        dist.barrier()
+    if not ready:
+        proc.kill()
+        raise SystemExit(f"rank {rank}: C5 host-resident child did not start")
+    out, _ = proc.communicate("go\n", timeout=600)
+    res = json.loads(out.strip().splitlines()[-1]) if proc.returncode == 0 else {"seconds": 0.0, "ok": False}
+    el, ok = float(res["seconds"]), bool(res["ok"])
+    if world > 1:
+        t = torch.tensor([el, 0.0 if ok else 1.0], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, ok = float(t[0].item()), t[1].item() == 0.0
+    if not ok:
+        raise SystemExit(f"rank {rank}: C5 host-resident round trip failed")
+    return {"gibs": int(lens_all.sum()) * steps / el / 2**30, "records_total": len(lens_all),
+            "bytes_total": int(lens_all.sum()), "seconds": el}
+
+
 def c5(args) -> dict:
     """mixed log-uniform 512 B-64 KiB records with the fused HMAC-SHA256 tag,
     starting and ending in pinned host memory, through the library's host pipeline
@@ -558,7 +654,7 @@ def c5(args) -> dict:
         dev, red_dev = dist_init(local)
     # BASELINE config 5: n = 524 288 records (~7 GB) unless --records says otherwise
     n_per = args.records if args.records_given else 524288
-    r = c5_host_timed(world, rank, dev.index, red_dev, n_per, args.c5_chunk_mib, args.c5_streams)
+    r = c5_host_child_timed(world, rank, dev.index, red_dev, n_per, args.c5_chunk_mib, args.c5_streams)
     res = None
     if rank == 0:
         res = {
@@ -570,6 +666,7 @@ def c5(args) -> dict:
             "config": {"workload": "C5", "records_total": r["records_total"], "bytes_total": r["bytes_total"],
                        "chunk_mib": args.c5_chunk_mib, "streams": args.c5_streams,
                        "host_buffers": "pinned", "host_mode": HOST_MODES[E.host_mode()],
+                       "hip_runtime": HOST_RUNTIME,
                        "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
     if world > 1:
@@ -795,6 +892,9 @@ def pow_bench(args) -> dict:
 
 def main():
     args = parse()
+    if args.host_child:
+        host_child_main(args)
+        return
     if args.mode == "pow":
         r = pow_bench(args)
         if r:
@@ -973,11 +1073,14 @@ def main():
     host = None
     if args.mode == "aead" and not args.no_host and (n, L) == (65536, 4096):
         import ephemeralnet_amd as E2
-        hc2 = host_c2(dev.index, n, L, 3, args.chunk_mib, args.streams)
-        hc5 = c5_host_timed(world, rank, dev.index, red_dev, 65536, args.c5_chunk_mib, args.c5_streams)
+        hc2 = host_c2_child(dev.index, n, L, args.chunk_mib, args.streams)
+        hc5 = c5_host_child_timed(world, rank, dev.index, red_dev, 65536, args.c5_chunk_mib, args.c5_streams)
+        hc2t = host_c2(dev.index, n, L, 3, args.chunk_mib, args.streams)  # this process: torch's runtime
         host = {"e2e_gibs": round(hc2["gibs"], 2), "e2e_seal_gibs": round(hc2["seal_gibs"], 2),
                 "e2e_open_gibs": round(hc2["open_gibs"], 2),
                 "e2e_is": "C2 (65 536 x 4 KiB) seal+open from and to pinned host memory, this rank",
+                "hip_runtime": HOST_RUNTIME,
+                "e2e_gibs_torch_hip_runtime": round(hc2t["gibs"], 2),
                 "c5_host_gibs": round(hc5["gibs"], 2),
                 "c5_host_is": f"BASELINE config 5 per-GPU share: {hc5['records_total']} log-uniform "
                               f"512 B-64 KiB records over {world} rank(s), AEAD + fused HMAC-SHA256 "
