@@ -611,9 +611,14 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     r.order = mixed ? reinterpret_cast<const uint32_t*>(sm + l.order) : nullptr;
     r.total_bytes_hint = in_b;
     r.max_len_hint = mx;
-    uint8_t* tags_out = sm + l.tags_out;
-    uint8_t* macs_out = sm + l.macs_out;
-    uint8_t* ok = sm + l.ok;
+    // the per-record outputs (tags, MACs, ok: <= 49 bytes a record) go straight from the kernel
+    // into the pinned host small block over PCIe: the down stream then carries only the arena
+    // copies (a small D2H behind every chunk's arena copy held the stream ~55 us per chunk,
+    // profiles/r04_c2_copy_trace_summary.jsonl)
+    uint8_t* smo = via_copies(md) ? s.small.d : sm;
+    uint8_t* tags_out = smo + l.tags_out;
+    uint8_t* macs_out = smo + l.macs_out;
+    uint8_t* ok = smo + l.ok;
     const uint8_t* tags_in = j.tags_in ? sm + l.tags_in : nullptr;
     const uint8_t* macs_in = j.macs_in ? sm + l.macs_in : nullptr;
     const uint8_t* ids = j.ids ? sm + l.ids : nullptr;
@@ -652,8 +657,6 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
     if (via_copies(md)) {
         uint8_t* h_out = s.direct_out ? j.out_base + j.out_off[s.c0] : s.out.h;
         if (s.out_b) hip_check(hipMemcpyAsync(h_out, s.d_out.p, s.out_b, hipMemcpyDeviceToHost, st), "D2H arena");
-        hip_check(hipMemcpyAsync(s.small.h + l.in_end, s.d_small.p + l.in_end, l.total - l.in_end,
-                                 hipMemcpyDeviceToHost, st), "D2H small");
     }
     hip_check(hipEventRecord(s.done, st), "hipEventRecord");
     s.busy = true;
