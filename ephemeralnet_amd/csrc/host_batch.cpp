@@ -545,22 +545,25 @@ void Engine::run_tasks(const Job& j, std::vector<CopyTask>& tasks) {
     pool().parallel(tasks.size(), [&](size_t t) {
         const CopyTask& c = tasks[t];
         uint64_t o = c.at;
+        // an arena's records [a, b) are one contiguous range (record i = [off[i], off[i+1])):
+        // one streaming copy instead of one per record
         if (c.kind == 0) {
+            if (j.in_spans.empty()) {
+                copy_out(c.base + o, j.in_base + j.in_off[c.a], j.in_off[c.b] - j.in_off[c.a]);
+            } else {
+                for (size_t i = c.a; i < c.b; ++i) {
+                    copy_out(c.base + o, in_ptr(j, i), lin_[i]);
+                    o += lin_[i];
+                }
+            }
+        } else if (j.out_vecs || !j.out_each.empty()) {
             for (size_t i = c.a; i < c.b; ++i) {
-                copy_out(c.base + o, in_ptr(j, i), lin_[i]);
-                o += lin_[i];
+                // assign from the range: one allocation and one copy, no zero fill first
+                vec_of(j, i).assign(c.base + o, c.base + o + lout_[i]);
+                o += lout_[i];
             }
         } else {
-            for (size_t i = c.a; i < c.b; ++i) {
-                const uint64_t len = lout_[i];
-                if (j.out_vecs || !j.out_each.empty()) {
-                    // assign from the range: one allocation and one copy, no zero fill first
-                    vec_of(j, i).assign(c.base + o, c.base + o + len);
-                } else {
-                    copy_out(j.out_base + j.out_off[i], c.base + o, len);
-                }
-                o += len;
-            }
+            copy_out(j.out_base + j.out_off[c.a], c.base + o, j.out_off[c.b] - j.out_off[c.a]);
         }
         fence_stores();  // streamed lines are globally visible before the device / caller reads them
     });
@@ -763,13 +766,15 @@ void Engine::run(const Job& j) {
         hip_check(hipStreamSynchronize(s0), "session setup");
     }
     // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
-    // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks.
+    // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
+    // (gathered C3 wire frames, 8 workers: 16 / 32 MiB -> 14.9 / 17.6 GiB/s,
+    // profiles/r04_batch_bench_c3_threads_chunks.jsonl).
     // Chain-bound jobs take 4x bigger chunks, so every chunk's kernel lasts at least its chain
     // (C5 share, 4 slots, two kernel streams: 128 / 256 MiB chunks -> 18.6 / 17.4 GiB/s,
     // profiles/r04_host_sweep_p7b.jsonl; one kernel stream peaked at 256 MiB).
     uint64_t chunk = cfg_.chunk_bytes;
     if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20) * chain)
-                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20) * std::min<uint64_t>(chain, 4));
+                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (32ull << 20) * std::min<uint64_t>(chain, 2));
     if (!cfg_.chunk_bytes)
         if (const char* e = std::getenv("ENET_HOST_CHUNK_MIB")) chunk = std::max(1ull, std::strtoull(e, nullptr, 10)) << 20;
     st_.jobs += 1;
