@@ -15,6 +15,9 @@ if [ "$PART" != b ]; then
 step pytest
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
 tail -2 $O/pytest_gpu.log
+step smoke
+timeout -k 10 240 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log
 step bench default
 timeout -k 10 240 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
