@@ -767,14 +767,14 @@ void Engine::run(const Job& j) {
     }
     // chunk size: big enough to amortise a launch, small enough that the gather / scatter of
     // neighbouring chunks overlaps it; a job with nothing to gather or scatter takes big chunks
-    // (gathered C3 wire frames, 8 workers: 16 / 32 MiB -> 14.9 / 17.6 GiB/s,
-    // profiles/r04_batch_bench_c3_threads_chunks.jsonl).
+    // (gathered records, 16 vs 32 MiB, three interleaved pairs on one box: C2 16.2-18.0 vs
+    // 13.8-17.5, C3 wire 14.9-16.4 vs 14.1-17.7 GiB/s, profiles/r04_batch_bench_gather_chunk_ab.jsonl).
     // Chain-bound jobs take 4x bigger chunks, so every chunk's kernel lasts at least its chain
     // (C5 share, 4 slots, two kernel streams: 128 / 256 MiB chunks -> 18.6 / 17.4 GiB/s,
     // profiles/r04_host_sweep_p7b.jsonl; one kernel stream peaked at 256 MiB).
     uint64_t chunk = cfg_.chunk_bytes;
     if (!chunk) chunk = (in_dev_ && direct_out) ? (md == Mode::ZeroCopy ? (256ull << 20) : (32ull << 20) * chain)
-                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (32ull << 20) * std::min<uint64_t>(chain, 2));
+                                                : (md == Mode::ZeroCopy ? (32ull << 20) : (16ull << 20) * std::min<uint64_t>(chain, 4));
     if (!cfg_.chunk_bytes)
         if (const char* e = std::getenv("ENET_HOST_CHUNK_MIB")) chunk = std::max(1ull, std::strtoull(e, nullptr, 10)) << 20;
     st_.jobs += 1;
