@@ -440,9 +440,10 @@ std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::
     if (message.size() + kMac > kMaxPayloadSize) return std::nullopt;  // SessionManager.cpp:358-360
     if (enet::scalar::g_policy.load() != ENET_SCALAR_DEVICE) {
         // host engine (policies auto and host): every session thread seals its own frame -- one
-        // MTU frame costs a core ~1 us, a device flush (pageable copies, launch, sync) ~170 us,
-        // so on the box the queue's device pass lost to this at 16 and 256 session threads
-        // (profiles/r03_frame_queue.jsonl); ENET_SCALAR_DEVICE batches on the MI355X
+        // MTU frame costs a core ~1 us, while a device pass cannot return before one lane's
+        // serial HMAC over the frame (~70 us), so on the box the queue's device passes lost to
+        // this at 16 and 256 session threads (profiles/r04_queue_bench.jsonl);
+        // ENET_SCALAR_DEVICE batches on the MI355X
         Nonce nonce;
         nonce_source().draw(nonce);
         enet::scalar::host_call();
