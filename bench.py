@@ -35,7 +35,7 @@ VALU_ISSUE_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, full-rate o
 WORKLOADS = {(65536, 4096): "C2", (1048576, 1500): "C3", (32768, 65536): "C4 (per-GPU share)"}
 METRIC = "GiB/s ChaCha20-Poly1305 seal+open (device-resident) at 1/2/4/8 MI355X"
 HOST_MODES = {0: "zero-copy kernels", 1: "SDMA per slot", 2: "SDMA split by direction",
-              3: "SDMA split by direction, kernels per slot"}
+              3: "SDMA split by direction, kernels per slot", 4: "SDMA in, kernels write host memory"}
 MODE_DESC = {"aead": "AEAD seal+open", "xor": "ChaCha20 xor twice",
              "wire": "wire frames (nonce||BE32||ChaCha20(m||HMAC)) seal+open",
              "store": "chunk store (SHA-256 id + ChaCha20) + fetch (decrypt + SHA-256 check)"}

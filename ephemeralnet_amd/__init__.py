@@ -378,7 +378,9 @@ def set_staging(variant: int) -> None:
 
 
 def set_host_mode(mode: int) -> None:
-    """Host-resident batches: 0 = zero-copy kernels on pinned host memory, 1 = SDMA copies."""
+    """Host-resident batches (enet_host_set_mode): 0 = zero-copy kernels on pinned host memory,
+    1 = SDMA copies per slot, 2 = copies split by direction, 3 = split with kernels on their own
+    streams (default), 4 = SDMA in, kernels writing host memory (no D2H copies)."""
     _check(lib().enet_host_set_mode(mode), "enet_host_set_mode")
 
 

@@ -313,6 +313,7 @@ Mode default_mode() {
         m = (e && std::strcmp(e, "sdma") == 0)    ? (int)Mode::Sdma
             : (e && std::strcmp(e, "split") == 0) ? (int)Mode::SdmaSplit
             : (e && std::strcmp(e, "zc") == 0)    ? (int)Mode::ZeroCopy
+            : (e && std::strcmp(e, "zcout") == 0) ? (int)Mode::SdmaInZcOut
                                                   : (int)Mode::SdmaSplitK;
         g_mode.store(m, std::memory_order_relaxed);
     }
@@ -344,7 +345,9 @@ bool trace_on() {
 double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-bool split_dirs(Mode m) { return m == Mode::SdmaSplit || m == Mode::SdmaSplitK; }
+bool split_dirs(Mode m) { return m == Mode::SdmaSplit || m == Mode::SdmaSplitK || m == Mode::SdmaInZcOut; }
+bool kern_streams(Mode m) { return m == Mode::SdmaSplitK || m == Mode::SdmaInZcOut; }
+bool zc_out(Mode m) { return m == Mode::SdmaInZcOut; }  // kernels write host memory, no D2H
 
 struct Slot {
     hipStream_t stream = nullptr;
@@ -419,12 +422,12 @@ private:
             return;
         }
         make(up_);
-        make(down_);
-        if (md == Mode::SdmaSplitK) {
+        if (!zc_out(md)) make(down_);
+        if (kern_streams(md)) {
             make(kern_[0]);
             if (chain) make(kern_[1]);
         }
-        nkern_ = (md == Mode::SdmaSplitK && chain) ? 2u : 1u;
+        nkern_ = (kern_streams(md) && chain) ? 2u : 1u;
     }
     Pool& pool() {
         if (!pool_) pool_ = std::make_unique<Pool>(worker_threads());
@@ -492,7 +495,7 @@ void Engine::stage(Slot& s, const Job& j, size_t c0, size_t c1, uint64_t in_b, u
     if (via_copies(md)) {
         s.d_small.ensure(s.lay.total);
         s.d_in.ensure(in_b);
-        s.d_out.ensure(out_b);
+        if (!zc_out(md)) s.d_out.ensure(out_b);
     }
     if (in_dev_) return;  // the caller's input arena is device-accessible: used in place
     s.in.ensure(in_b);
@@ -586,14 +589,15 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         const uint8_t* h_in = in_dev_ ? in_ptr(j, s.c0) : src_in;
         if (in_b) hip_check(hipMemcpyAsync(s.d_in.p, h_in, in_b, hipMemcpyHostToDevice, st), "H2D arena");
         hip_check(hipMemcpyAsync(s.d_small.p, s.small.h, l.in_end, hipMemcpyHostToDevice, st), "H2D small");
-        if (md == Mode::SdmaSplitK) {
+        if (kern_streams(md)) {
             hip_check(hipEventRecord(s.indone, st), "hipEventRecord");
             // two kernel streams for hash-chain-bound jobs: consecutive chunks' chains overlap
             st = kern_[nkern_ > 1 ? (s.seq & 1) : 0];
             hip_check(hipStreamWaitEvent(st, s.indone, 0), "hipStreamWaitEvent");
         }
         din = s.d_in.p;
-        dout = s.d_out.p;
+        // SdmaInZcOut: outputs straight into the caller's arena (device view) or the pinned staging
+        dout = !zc_out(md) ? s.d_out.p : s.direct_out ? out_dev_ + j.out_off[s.c0] : s.out.d;
         sm = s.d_small.p;
     } else {
         din = in_dev_ ? in_dev_ + j.in_off[s.c0] : s.in.d;
@@ -652,12 +656,12 @@ void Engine::launch(Slot& s, const Job& j, uint64_t in_b, uint32_t mx, bool mixe
         case Op::ChunkStore: enet_check(enet_chunk_store_batch(&r, ids, macs_out, st), "chunk_store"); break;
         case Op::ChunkFetch: enet_check(enet_chunk_fetch_batch(&r, ids, macs_in, ok, st), "chunk_fetch"); break;
     }
-    if (split_dirs(md)) {
+    if (split_dirs(md) && !zc_out(md)) {
         hip_check(hipEventRecord(s.kdone, st), "hipEventRecord");
         st = down_;
         hip_check(hipStreamWaitEvent(st, s.kdone, 0), "hipStreamWaitEvent");
     }
-    if (via_copies(md)) {
+    if (via_copies(md) && !zc_out(md)) {
         uint8_t* h_out = s.direct_out ? j.out_base + j.out_off[s.c0] : s.out.h;
         if (s.out_b) hip_check(hipMemcpyAsync(h_out, s.d_out.p, s.out_b, hipMemcpyDeviceToHost, st), "D2H arena");
     }

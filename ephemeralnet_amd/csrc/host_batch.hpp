@@ -82,7 +82,12 @@ struct Job {
 //               on "down", events between them, so neither copy direction ever waits behind a
 //               kernel, consecutive chunks' hash chains (~2 ms per launch for 64 KiB records)
 //               overlap, and no two streams share one of the box's four hardware queues
-enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2, SdmaSplitK = 3 };
+// ZeroCopy: kernels read and write pinned host memory; Sdma: H2D / kernel / D2H per slot stream;
+// SdmaSplit: every H2D + kernel on one stream, every D2H on another; SdmaSplitK: H2D on one
+// stream, kernels on their own (two for hash-chain-bound jobs), D2H on a third; SdmaInZcOut: H2D
+// by SDMA as SdmaSplitK, but the kernels write their outputs straight into pinned host memory (no
+// D2H copies at all)
+enum class Mode : int { ZeroCopy = 0, Sdma = 1, SdmaSplit = 2, SdmaSplitK = 3, SdmaInZcOut = 4 };
 
 struct Config {
     uint64_t chunk_bytes = 0;  // 0: the mode's default

@@ -228,9 +228,10 @@ int enet_pipeline_wire_open(enet_pipeline* p, const enet_records* r, uint8_t* ok
 }
 
 int enet_host_set_mode(int mode) {
-    if (mode < 0 || mode > 3) {
+    if (mode < 0 || mode > 4) {
         enet::set_last_error("enet_host_set_mode: mode must be 0 (zero-copy), 1 (SDMA copies), 2 (SDMA, one "
-                             "stream per direction) or 3 (SDMA per direction, kernels per slot)");
+                             "stream per direction), 3 (SDMA per direction, kernels on their own streams) "
+                             "or 4 (SDMA in, kernels write host memory)");
         return ENET_EINVAL;
     }
     enet::hb::set_default_mode((enet::hb::Mode)mode);

@@ -21,7 +21,7 @@ def enet():
     yield E
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["zerocopy", "sdma", "sdma_split", "sdma_split_k"])
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["zerocopy", "sdma", "sdma_split", "sdma_split_k", "sdma_in_zc_out"])
 def mode(enet, request):
     """Both ways the host runtime reaches host memory (enet_host_set_mode): zero-copy kernels on
     pinned staging, and SDMA copies into device arenas.  Same bytes either way."""

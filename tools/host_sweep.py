@@ -12,7 +12,7 @@ import bench  # noqa: E402
 import ephemeralnet_amd as E  # noqa: E402
 
 which = sys.argv[1] if len(sys.argv) > 1 else "all"
-MODES = {"zc": 0, "sdma": 1, "split": 2, "splitk": 3}
+MODES = {"zc": 0, "sdma": 1, "split": 2, "splitk": 3, "zcout": 4}
 if which in ("c2one", "c5one"):  # one configuration from the environment (for a trace)
     m, slots, chunk = os.environ.get("ONE", "splitk,3,256").split(",")
     E.set_host_mode(MODES[m])
