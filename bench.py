@@ -567,6 +567,7 @@ def host_child_main(args) -> None:
     E.lib()  # before torch: the system HIP runtime
     if args.host_child == "c2":
         r = host_c2(args.host_device, args.records, args.record_bytes, 3, args.chunk_mib, args.streams)
+        r["host_mode"] = E.host_mode()
         print(json.dumps(r), flush=True)
         return
     lens = c5_lengths(args.c5_all)[args.c5_lo:args.c5_hi]
@@ -579,7 +580,8 @@ def host_child_main(args) -> None:
     for _ in range(args.c5_steps):
         step()
     el = time.perf_counter() - t0
-    print(json.dumps({"seconds": el, "ok": bool(check()), "bytes": int(mine)}), flush=True)
+    print(json.dumps({"seconds": el, "ok": bool(check()), "bytes": int(mine), "host_mode": E.host_mode()}),
+          flush=True)
 
 
 def host_child(kind: str, dev_index: int, extra: list):
@@ -633,7 +635,7 @@ def c5_host_child_timed(world: int, rank: int, dev_index: int, red_dev, n_per_ra
     if not ok:
         raise SystemExit(f"rank {rank}: C5 host-resident round trip failed")
     return {"gibs": int(lens_all.sum()) * steps / el / 2**30, "records_total": len(lens_all),
-            "bytes_total": int(lens_all.sum()), "seconds": el}
+            "bytes_total": int(lens_all.sum()), "seconds": el, "host_mode": res.get("host_mode", 3)}
 
 
 def c5(args) -> dict:
@@ -643,8 +645,6 @@ def c5(args) -> dict:
     (shard.py), no collective."""
     import torch
     import torch.distributed as dist
-
-    import ephemeralnet_amd as E
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -665,7 +665,7 @@ def c5(args) -> dict:
             "n_gpus": world,
             "config": {"workload": "C5", "records_total": r["records_total"], "bytes_total": r["bytes_total"],
                        "chunk_mib": args.c5_chunk_mib, "streams": args.c5_streams,
-                       "host_buffers": "pinned", "host_mode": HOST_MODES[E.host_mode()],
+                       "host_buffers": "pinned", "host_mode": HOST_MODES[r["host_mode"]],
                        "hip_runtime": HOST_RUNTIME,
                        "path": "enet_pipeline_aead_hmac_seal/open (libenet_crypto.so)"},
         }
@@ -1081,11 +1081,12 @@ def main():
                 "e2e_is": "C2 (65 536 x 4 KiB) seal+open from and to pinned host memory, this rank",
                 "hip_runtime": HOST_RUNTIME,
                 "e2e_gibs_torch_hip_runtime": round(hc2t["gibs"], 2),
+                "host_mode_torch_hip_runtime": HOST_MODES[E2.host_mode()],
                 "c5_host_gibs": round(hc5["gibs"], 2),
                 "c5_host_is": f"BASELINE config 5 per-GPU share: {hc5['records_total']} log-uniform "
                               f"512 B-64 KiB records over {world} rank(s), AEAD + fused HMAC-SHA256 "
                               "seal+open, pinned host memory in and out, all ranks' bytes / max-over-ranks time",
-                "host_mode": HOST_MODES[E2.host_mode()],
+                "host_mode": HOST_MODES[hc2.get("host_mode", 3)],
                 "path": "enet_pipeline_aead_* / enet_pipeline_aead_hmac_* (host_batch.cpp)"}
 
     if rank == 0:

@@ -307,14 +307,23 @@ Mode default_mode() {
     int m = g_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char* e = std::getenv("ENET_HOST_MODE");
-        // default: copies split by direction with per-slot kernels -- measured best for uniform
-        // (C2 e2e 18.4-19.1 GiB/s) and mixed HMAC batches (C5 share 15.9) alike
-        // (profiles/r04_host_sweep_*.jsonl); zero-copy kernels reach 13-16
+        // default: copies split by direction, kernels on their own streams -- measured best on
+        // the HIP runtime the library is built against, for uniform (C2 e2e 19.0-19.4 GiB/s) and
+        // mixed HMAC batches (C5 share 18.7) alike; kernels writing host memory (mode 4) reach
+        // 15.8-18.0 / 15.3-15.7 there.  On any other HIP runtime (in practice PyTorch's bundled
+        // one, when torch is imported before the library) every D2H hipMemcpyAsync runs as a blit
+        // kernel (profiles/r04_torch_runtime_host_c2_*_stats.csv): there mode 4, with no D2H
+        // copies, measured 17.9 against 14.0-14.3 (profiles/r04_host_mode4.jsonl)
+        int v = 0;
+        const bool own_runtime = hipRuntimeGetVersion(&v) == hipSuccess && v / 10000000 == HIP_VERSION_MAJOR &&
+                                 (v / 100000) % 100 == HIP_VERSION_MINOR;
         m = (e && std::strcmp(e, "sdma") == 0)    ? (int)Mode::Sdma
             : (e && std::strcmp(e, "split") == 0) ? (int)Mode::SdmaSplit
             : (e && std::strcmp(e, "zc") == 0)    ? (int)Mode::ZeroCopy
             : (e && std::strcmp(e, "zcout") == 0) ? (int)Mode::SdmaInZcOut
-                                                  : (int)Mode::SdmaSplitK;
+            : (e && std::strcmp(e, "splitk") == 0) ? (int)Mode::SdmaSplitK
+            : own_runtime                          ? (int)Mode::SdmaSplitK
+                                                   : (int)Mode::SdmaInZcOut;
         g_mode.store(m, std::memory_order_relaxed);
     }
     return (Mode)m;
