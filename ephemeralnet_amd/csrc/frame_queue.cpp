@@ -21,6 +21,7 @@
 #include <functional>
 #include <future>
 #include <thread>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -247,8 +248,17 @@ public:
         std::lock_guard<std::mutex> lk(mu_);
         auto& e = e_[w % e_.size()];
         if (!e) {
+            // a pass is a few hundred KiB at most and latency-bound: by default the kernels read
+            // and write the pinned staging directly (zero-copy, one stream, no copies);
+            // ENET_QUEUE_HOST_MODE=0..4 picks another host mode (enet_host_set_mode)
+            static const int qmode = [] {
+                const char* v = std::getenv("ENET_QUEUE_HOST_MODE");
+                const int m = v ? std::atoi(v) : 0;
+                return m >= 0 && m <= 4 ? m : 0;
+            }();
             enet::hb::Config cfg;
             cfg.slots = 1;
+            cfg.mode = qmode;
             e = enet::hb::create_engine(dev_, cfg);
         }
         return *e;
