@@ -808,8 +808,12 @@ void Engine::run(const Job& j) {
             // (not at the end when the chunk's kernel is a long hash chain: each extra chunk
             // costs one more ~2 ms chain after the copies are done)
             uint64_t target = chunk;
-            if (k < 3) target = std::max<uint64_t>(chunk >> (3 - k), 1);
-            if (left < 2 * chunk && chain == 1)
+            static const unsigned ramp = [] {  // ENET_HOST_RAMP: bit 0 ramp-up, bit 1 ramp-down (tuning)
+                const char* e = std::getenv("ENET_HOST_RAMP");
+                return e ? (unsigned)std::strtoul(e, nullptr, 10) & 3u : 3u;
+            }();
+            if (k < 3 && (ramp & 1u)) target = std::max<uint64_t>(chunk >> (3 - k), 1);
+            if (left < 2 * chunk && chain == 1 && (ramp & 2u))
                 target = std::min<uint64_t>(target, std::max<uint64_t>(left / 2, chunk >> 3));
             size_t c1 = c0 + 1;
             uint64_t ib = lin_[c0], ob = lout_[c0];
