@@ -802,15 +802,17 @@ void Engine::run(const Job& j) {
     uint64_t left = in_total;
     try {
         while (c0 < n) {
-            // ramped chunk sizes: the first chunks (nothing to overlap their copy in yet) and
-            // the last ones (nothing left to overlap their copy out) are small, 1/8 .. 1/2 of the
-            // steady chunk, so the pipeline fills and drains in a fraction of a chunk's time
-            // (not at the end when the chunk's kernel is a long hash chain: each extra chunk
-            // costs one more ~2 ms chain after the copies are done)
+            // ramped chunk sizes: the first chunks (nothing to overlap their copy in yet) are
+            // small, 1/8 .. 1/2 of the steady chunk, so the pipeline fills in a fraction of a
+            // chunk's time.  Ramping down at the end as well measured ~1 % slower (every extra
+            // chunk pays its small copies and event hops; C2 e2e 19.1-19.3 vs 19.46, four
+            // interleaved pairs, profiles/r04_host_ramp_ab.jsonl) and costs a hash-chain-bound
+            // job one more ~2 ms chain per extra chunk, so it is off by default.
+            // ENET_HOST_RAMP (tuning): bit 0 ramp-up, bit 1 ramp-down for unhashed jobs.
             uint64_t target = chunk;
-            static const unsigned ramp = [] {  // ENET_HOST_RAMP: bit 0 ramp-up, bit 1 ramp-down (tuning)
+            static const unsigned ramp = [] {
                 const char* e = std::getenv("ENET_HOST_RAMP");
-                return e ? (unsigned)std::strtoul(e, nullptr, 10) & 3u : 3u;
+                return e ? (unsigned)std::strtoul(e, nullptr, 10) & 3u : 1u;
             }();
             if (k < 3 && (ramp & 1u)) target = std::max<uint64_t>(chunk >> (3 - k), 1);
             if (left < 2 * chunk && chain == 1 && (ramp & 2u))
