@@ -808,14 +808,15 @@ void Engine::run(const Job& j) {
             // chunk pays its small copies and event hops; C2 e2e 19.1-19.3 vs 19.46, four
             // interleaved pairs, profiles/r04_host_ramp_ab.jsonl) and costs a hash-chain-bound
             // job one more ~2 ms chain per extra chunk, so it is off by default.
-            // ENET_HOST_RAMP (tuning): bit 0 ramp-up, bit 1 ramp-down for unhashed jobs.
+            // ENET_HOST_RAMP (tuning): bit 0 ramp-up, bit 1 ramp-down for unhashed jobs, bit 2
+            // ramp-down for hash-chain-bound jobs.
             uint64_t target = chunk;
             static const unsigned ramp = [] {
                 const char* e = std::getenv("ENET_HOST_RAMP");
-                return e ? (unsigned)std::strtoul(e, nullptr, 10) & 3u : 1u;
+                return e ? (unsigned)std::strtoul(e, nullptr, 10) & 7u : 1u;
             }();
             if (k < 3 && (ramp & 1u)) target = std::max<uint64_t>(chunk >> (3 - k), 1);
-            if (left < 2 * chunk && chain == 1 && (ramp & 2u))
+            if (left < 2 * chunk && (ramp & (chain == 1 ? 2u : 4u)))
                 target = std::min<uint64_t>(target, std::max<uint64_t>(left / 2, chunk >> 3));
             size_t c1 = c0 + 1;
             uint64_t ib = lin_[c0], ob = lout_[c0];
