@@ -807,7 +807,8 @@ void Engine::run(const Job& j) {
             // chunk's time.  Ramping down at the end as well measured ~1 % slower (every extra
             // chunk pays its small copies and event hops; C2 e2e 19.1-19.3 vs 19.46, four
             // interleaved pairs, profiles/r04_host_ramp_ab.jsonl) and costs a hash-chain-bound
-            // job one more ~2 ms chain per extra chunk, so it is off by default.
+            // job one more ~2 ms chain per extra chunk (C5 share 17.6-17.8 vs 18.4-18.6,
+            // r04_host_ramp_c5_ab.jsonl), so it is off by default.
             // ENET_HOST_RAMP (tuning): bit 0 ramp-up, bit 1 ramp-down for unhashed jobs, bit 2
             // ramp-down for hash-chain-bound jobs.
             uint64_t target = chunk;
