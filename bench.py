@@ -78,6 +78,10 @@ def parse():
     ap.add_argument("--c5-steps", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--no-pin", action="store_true",
                     help="do not pin this rank (and its host children) to its GPU's NUMA node CPUs")
+    ap.add_argument("--no-long", action="store_true",
+                    help="skip the long-record side leg (1 x 32 MiB, 8 x 1 MiB)")
+    ap.add_argument("--long-only", action="store_true",
+                    help="print only the long-record side leg (device-resident) and exit")
     ap.add_argument("--no-host", action="store_true",
                     help="default line: skip the host-resident extra keys (C2 e2e, C5 per-GPU share)")
     ap.add_argument("--c5-chunk-mib", type=int, default=0,
@@ -997,6 +1001,64 @@ def pow_bench(args) -> dict:
     return out
 
 
+def long_records_leg(dev, reps: int = 20) -> dict:
+    """Side leg (never `value`): the reference's real chunk sizes, device-resident -- a stored file
+    is ONE chunk of up to 32 MiB (Config.hpp:62, Node.cpp:1414-1417) and session payloads go up
+    to 1 MiB (SessionManager.cpp:87).  AEAD seal+open and ChaCha20 (XOR, both directions) GiB/s =
+    plaintext bytes per seal+open pair / its HIP-event time, on the sequence-parallel tiles
+    (segments.hip) and, for comparison, on the record engine alone (16 lanes per record)."""
+    import numpy as np
+    import torch
+    import ephemeralnet_amd as E
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for name, lens in (("1x32MiB", [32 << 20]), ("8x1MiB", [1 << 20] * 8)):
+        n, tot = len(lens), sum(lens)
+        g = torch.Generator(device=dev).manual_seed(77)
+        pt = torch.randint(0, 256, (tot,), dtype=torch.uint8, device=dev, generator=g)
+        keys = torch.randint(0, 256, (32 * n,), dtype=torch.uint8, device=dev, generator=g)
+        nonces = torch.randint(0, 256, (12 * n,), dtype=torch.uint8, device=dev, generator=g)
+        offs = torch.tensor([0] + list(np.cumsum(lens)), dtype=torch.int64, device=dev)
+        ct, back = torch.empty_like(pt), torch.empty_like(pt)
+        tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+        ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+        sb = E.Batch(pt, offs, keys, nonces, total_bytes_hint=tot, max_len_hint=max(lens))
+        ob = E.Batch(ct, offs, keys, nonces, total_bytes_hint=tot, max_len_hint=max(lens))
+        row = {}
+        for path, seg in (("tiles", -1), ("record_engine", E.SEG_NEVER)):
+            E.set_seg_min(seg)
+            for mode in ("aead", "xor"):
+                def pair():
+                    if mode == "aead":
+                        E.aead_seal(sb, ct, tags, stream=stream)
+                        E.aead_open(ob, back, tags, ok, stream=stream)
+                    else:
+                        E.chacha20_xor(sb, ct, stream=stream)
+                        E.chacha20_xor(ob, back, stream=stream)
+                r_ = reps if path == "tiles" else max(2, reps // 10)
+                for _ in range(3):
+                    pair()
+                torch.cuda.synchronize(dev)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                ev[0].record(stream)
+                for _ in range(r_):
+                    pair()
+                ev[1].record(stream)
+                ev[1].synchronize()
+                ms = ev[0].elapsed_time(ev[1]) / r_
+                good = torch.equal(back, pt) and not torch.equal(ct, pt) and (
+                    mode == "xor" or int(ok.sum()) == n)
+                row[f"{mode}_{path}_gibs"] = round(tot / (ms * 1e-3) / 2**30, 1)
+                row[f"{mode}_{path}_ms"] = round(ms, 4)
+                row[f"{mode}_{path}_ok"] = bool(good)
+        E.set_seg_min(-1)
+        res[name] = row
+    res["is"] = ("device-resident, per-record (key, nonce); GiB/s = plaintext bytes / (seal + open) "
+                 "time; tiles = 64 KiB tiles over every CU (default), record_engine = at most 16 lanes "
+                 "per record (enet_set_seg_min(INT64_MAX))")
+    return res
+
+
 def main():
     args = parse()
     if args.host_child:
@@ -1018,6 +1080,12 @@ def main():
         return
     if args.e2e:
         print(json.dumps(e2e(args)), flush=True)
+        return
+    if args.long_only:
+        import torch
+        import ephemeralnet_amd as E
+        E.lib()
+        print(json.dumps({"long_records": long_records_leg(torch.device("cuda", 0))}), flush=True)
         return
     sampler = None
     if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_power
@@ -1203,6 +1271,9 @@ def main():
             fq = frame_queue_leg(dev.index)
             if fq is not None:
                 host["frame_queue"] = fq
+    long_recs = None
+    if args.mode == "aead" and world == 1 and not args.no_long and (n, L) == (65536, 4096):
+        long_recs = long_records_leg(dev)
     # every rank's placement (node, CPUs, CPU share) and its C5 share's pinned bytes / staging node
     placements = gather_placement(world, {**PLACEMENT_SHORT(), "c5_host": host.get("c5_host") if host else None})
     if ranks is not None and placements is not None:
@@ -1319,6 +1390,10 @@ def main():
         }
         if power:
             out["power"] = power
+        if long_recs:
+            long_recs["vs_c2_value"] = {k: round(v["aead_tiles_gibs"] / value, 3)
+                                        for k, v in long_recs.items() if isinstance(v, dict)}
+            out["long_records"] = long_recs
         if host:
             out["host_resident"] = host
         out["placement"] = PLACEMENT

@@ -58,7 +58,7 @@ EXPORTS = [
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split",
-    "enet_last_error",
+    "enet_set_seg_min", "enet_seg_batches", "enet_last_error",
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
     "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_pipeline_wire_seal",
@@ -157,6 +157,8 @@ def lib() -> C.CDLL:
         L.enet_set_lanes_per_record.argtypes = [u32]
         L.enet_set_staging.argtypes = [C.c_int]
         L.enet_set_duplex_split.argtypes = [C.c_int]
+        L.enet_set_seg_min.argtypes = [C.c_int64]
+        L.enet_seg_batches.restype = C.c_uint64
         L.enet_last_error.restype = C.c_char_p
         L.enet_pipeline_create.argtypes = [C.c_int, u64, u32]
         L.enet_pipeline_create.restype = vp
@@ -257,6 +259,20 @@ class Batch:
         r.total_bytes_hint = self.total_bytes_hint
         r.max_len_hint = self.max_len_hint
         return r
+
+
+def set_seg_min(nbytes: int) -> None:
+    """enet_set_seg_min: -1 automatic; >= 0 every record of at least nbytes takes the
+    sequence-parallel tiles (segments.hip); 2**63-1 never."""
+    _check(lib().enet_set_seg_min(int(nbytes)), "enet_set_seg_min")
+
+
+def seg_batches() -> int:
+    return int(lib().enet_seg_batches())
+
+
+SEG_MIN = 256 << 10
+SEG_NEVER = (1 << 63) - 1
 
 
 def chacha20_xor(b: Batch, out, counters=None, out_offsets=None, stream=None) -> None:

@@ -21,7 +21,7 @@ OBJ = os.path.join(PKG, "build")
 # variants selectable from the environment); loaded only through ENET_LIB_PATH by tools/
 LIB_TOOLS = os.path.join(PKG, "libenet_crypto_tools.so")
 OBJ_TOOLS = os.path.join(PKG, "build_tools")
-SOURCES = ["records.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "duplex_split.hip",
+SOURCES = ["records.hip", "segments.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "duplex_split.hip",
            "capi.cpp", "crypto_api.cpp", "pipeline.cpp", "host_engine.cpp", "frame_queue.cpp", "host_batch.cpp",
            "host_topo.cpp"]
 HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "stream_common.hpp", "host_engine.hpp",

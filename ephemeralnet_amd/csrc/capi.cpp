@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "enet_internal.hpp"
@@ -149,6 +150,126 @@ uint32_t lanes_for(const enet_records* r) {
     return enet::choose_lanes(r->count, r->total_bytes_hint, r->max_len_hint);
 }
 
+// ---- the sequence-parallel path (segments.hip) for long records
+// -1: auto (below); otherwise every record of at least this many bytes takes the tiles, whatever
+// the hints say (enet_set_seg_min: tests / tuning; INT64_MAX = never)
+std::atomic<int64_t> g_seg_min{-1};
+std::atomic<uint64_t> g_seg_batches{0};  // batches that took the tiles (enet_seg_batches)
+
+// Auto: a batch whose longest record (hint) is >= kSegMin takes the tiles for its records >=
+// kSegMin -- unless it is uniform and wide enough that 16 lanes per record already fill the chip
+// (n * 16 >= 131 072 lanes: the record / streaming kernels run those at the C2 rate).
+bool seg_wanted(const enet_records* r, uint64_t& long_min) {
+    const int64_t f = g_seg_min.load(std::memory_order_relaxed);
+    if (f >= 0) {
+        long_min = (uint64_t)f;
+        return f != INT64_MAX;
+    }
+    long_min = enet::kSegMin;
+    if (r->max_len_hint < enet::kSegMin) return false;
+    const bool uniform = r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint;
+    return !(uniform && (uint64_t)r->count * enet::kMaxLanesPerRecord >= 131072u);
+}
+
+// Scratch comes from a library-private, stream-ordered pool per device (hipMallocFromPoolAsync /
+// hipFreeAsync on the caller's stream): no synchronisation, capturable, and concurrent calls on
+// different streams get their own.  Freed memory stays in the pool.
+hipMemPool_t seg_pool() {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pools[dev]) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        hipMemPool_t pl = nullptr;
+        if (hipMemPoolCreate(&pl, &props) != hipSuccess) return nullptr;
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pl, hipMemPoolAttrReleaseThreshold, &keep);
+        pools[dev] = pl;
+    }
+    return pools[dev];
+}
+
+struct SegRun {
+    void* mem = nullptr;
+    const uint8_t* claimed = nullptr;
+};
+
+// Plan + tile kernels for the batch's long records; sr.claimed marks them for the record engine
+int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long_min, hipStream_t st,
+              SegRun& sr) {
+    const uint32_t n = r->count;
+    const uint64_t total = r->total_bytes_hint ? r->total_bytes_hint
+                                               : (uint64_t)std::min<uint32_t>(n, 1024u) * r->max_len_hint;
+    // capacities from the hints; records past them stay with the record engine (never wrong bytes)
+    const uint64_t ecap = std::min<uint64_t>(n, long_min ? total / long_min + 1 : n);
+    const uint64_t tcap = std::min<uint64_t>(total / enet::kSegTileBytes + ecap + 1, 0xFFFFFFFFull);
+    const size_t o_ent = 256, o_cl = o_ent + (size_t)ecap * sizeof(enet::SegEntry),
+                 o_part = (o_cl + n + 255) & ~size_t(255), bytes = o_part + (size_t)tcap * 32;
+    hipMemPool_t pool = seg_pool();
+    if (!pool) return fail(ENET_EHIP, "sequence-parallel scratch: no memory pool for the current device");
+    if (hipError_t e = hipMallocFromPoolAsync(&sr.mem, bytes, pool, st)) {
+        sr.mem = nullptr;
+        return hip_status(e, "sequence-parallel scratch");
+    }
+    uint8_t* base = static_cast<uint8_t*>(sr.mem);
+    enet::SegParams q{};
+    q.mode = mode;
+    q.n = n;
+    q.in_off = p.in_off;
+    q.out_off = p.out_off;
+    q.in = p.in;
+    q.out = p.out;
+    q.keys = p.keys;
+    q.key_stride = p.key_stride;
+    q.nonces = p.nonces;
+    q.counters = p.counters;
+    q.counter_stride = p.counter_stride;
+    q.aad = p.aad;
+    q.aad_off = p.aad_off;
+    q.tag_in = p.tag_in;
+    q.tag_out = p.tag_out;
+    q.ok = p.ok;
+    q.hdr = reinterpret_cast<unsigned long long*>(base);
+    q.entries = reinterpret_cast<enet::SegEntry*>(base + o_ent);
+    q.claimed = base + o_cl;
+    q.partials = reinterpret_cast<uint32_t*>(base + o_part);
+    q.entry_cap = (uint32_t)ecap;
+    q.tile_cap = (uint32_t)tcap;
+    q.long_min = long_min;
+    const uint32_t plan_blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 1024);
+    const uint32_t tile_blocks = (uint32_t)std::min<uint64_t>(tcap, 4096);
+    sr.claimed = q.claimed;
+    g_seg_batches.fetch_add(1, std::memory_order_relaxed);
+    return hip_status(enet::launch_seg(q, plan_blocks, tile_blocks, st), "sequence-parallel launch");
+}
+
+void seg_end(SegRun& sr, hipStream_t st) {
+    if (sr.mem) (void)hipFreeAsync(sr.mem, st);
+    sr.mem = nullptr;
+}
+
+// The record engine over the batch, with the long records on the tiles first when seg_wanted
+int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t st, const char* what) {
+    uint64_t long_min = 0;
+    SegRun sr;
+    if (mode <= enet::MODE_OPEN && seg_wanted(r, long_min)) {
+        if (int e = seg_begin(mode, r, p, long_min, st, sr)) {
+            seg_end(sr, st);
+            return e;
+        }
+        p.skip = sr.claimed;
+        p.uniform_len = 0;  // per-lane path: the staged paths assume every record is theirs
+    }
+    const int rc = hip_status(enet::launch_records(mode, p, lanes_for(r), st), what);
+    seg_end(sr, st);
+    return rc;
+}
+
 }  // namespace
 
 namespace enet {
@@ -230,6 +351,14 @@ int enet_set_duplex_split(int mode) {
     return ENET_OK;
 }
 
+int enet_set_seg_min(int64_t bytes) {
+    if (bytes < -1) return fail(ENET_EINVAL, "seg_min must be -1 (auto), 0 .. INT64_MAX");
+    g_seg_min.store(bytes, std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+uint64_t enet_seg_batches(void) { return g_seg_batches.load(std::memory_order_relaxed); }
+
 int enet_set_lanes_per_record(uint32_t lanes) {
     if (lanes != 0 && lanes != 1 && lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16)
         return fail(ENET_EINVAL, "lanes must be 0, 1, 2, 4, 8 or 16");
@@ -243,8 +372,7 @@ int enet_chacha20_xor_batch(const enet_records* r, const uint32_t* counters, voi
     if (counters && !aligned4(counters)) return fail(ENET_EINVAL, "counters misaligned");
     enet::RecParams p = rec_params(r);
     p.counters = counters;
-    return hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), (hipStream_t)stream),
-                      "chacha20_xor launch");
+    return run_records(enet::MODE_XOR, r, p, (hipStream_t)stream, "chacha20_xor launch");
 }
 
 int enet_aead_seal_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
@@ -258,8 +386,7 @@ int enet_aead_seal_batch(const enet_records* r, const uint8_t* aad, const uint64
     p.aad = aad;
     p.aad_off = aad_offsets;
     p.tag_out = tags;
-    return hip_status(enet::launch_records(enet::MODE_SEAL, p, lanes_for(r), (hipStream_t)stream),
-                      "aead_seal launch");
+    return run_records(enet::MODE_SEAL, r, p, (hipStream_t)stream, "aead_seal launch");
 }
 
 int enet_aead_open_batch(const enet_records* r, const uint8_t* aad, const uint64_t* aad_offsets,
@@ -274,8 +401,7 @@ int enet_aead_open_batch(const enet_records* r, const uint8_t* aad, const uint64
     p.aad_off = aad_offsets;
     p.tag_in = tags;
     p.ok = ok;
-    return hip_status(enet::launch_records(enet::MODE_OPEN, p, lanes_for(r), (hipStream_t)stream),
-                      "aead_open launch");
+    return run_records(enet::MODE_OPEN, r, p, (hipStream_t)stream, "aead_open launch");
 }
 
 int enet_sha256_batch(uint32_t n, const uint8_t* in, const uint64_t* offsets, uint8_t* digests,

@@ -53,6 +53,9 @@ struct RecParams {
     // nonce(12) || BE32(|body|) (SessionManager.cpp:376-387).  Seal writes it in front of the
     // body; open reads the nonce from it.
     uint32_t hdr;
+    // records the sequence-parallel path (segments.hip) claimed: skip[rec] != 0 -> not this
+    // kernel's record (nullable; per-lane path only)
+    const uint8_t* skip;
 };
 
 // lanes: 1, 2, 4, 8 or 16 lanes per record.
@@ -154,6 +157,44 @@ hipError_t launch_hmac_midstates(uint32_t n, const uint8_t* keys, uint32_t* mid,
 hipError_t launch_session_keys(uint32_t n, const uint8_t* secrets, const uint64_t* counters,
                                const int64_t* ticks, uint8_t* out, hipStream_t s);
 
+
+// ---- sequence-parallel path for long records (segments.hip)
+// A claimed record's entry; entries are sorted by tile_base (claimed by CAS on one packed word).
+struct SegEntry {
+    uint32_t rec, tile_base, ntiles, arrived;
+    uint32_t aad_len, nbits, pad0, pad1;
+    uint32_t r[4], s[4];     // AEAD: one-time key halves (r unclamped words; s the pad)
+    uint32_t pw[5 * 40];     // AEAD: r^(2^k) in 26-bit limbs, k < nbits
+};
+constexpr uint64_t kSegMin = 256u << 10;   // records this long take the tiles (seg_wanted)
+constexpr uint64_t kSegTileBytes = 64u << 10;
+constexpr uint64_t kSegMaxLen = 1ull << 35;  // 32-bit Poly1305 block positions inside a record
+struct SegParams {
+    int mode;                  // MODE_XOR / MODE_SEAL / MODE_OPEN
+    uint32_t n;
+    const uint64_t* in_off;
+    const uint64_t* out_off;
+    const uint8_t* in;
+    uint8_t* out;
+    const uint8_t* keys;
+    uint32_t key_stride;
+    const uint8_t* nonces;
+    const uint32_t* counters;  // MODE_XOR start counters (nullable -> 0)
+    uint32_t counter_stride;
+    const uint8_t* aad;
+    const uint64_t* aad_off;
+    const uint8_t* tag_in;
+    uint8_t* tag_out;
+    uint8_t* ok;
+    // scratch (stream-ordered, capi.cpp seg_begin)
+    unsigned long long* hdr;   // count << 40 | tiles claimed
+    SegEntry* entries;         // [entry_cap]
+    uint8_t* claimed;          // [n]
+    uint32_t* partials;        // [tile_cap][8]
+    uint32_t entry_cap, tile_cap;
+    uint64_t long_min;
+};
+hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_blocks, hipStream_t s);
 
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
 uint32_t staging_variant();

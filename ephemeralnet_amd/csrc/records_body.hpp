@@ -130,8 +130,22 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
     const uint32_t gid = blockIdx.x * WGS + threadIdx.x;
     const uint32_t group = gid >> LOGP;
     const uint32_t j = gid & (P - 1);
-    const bool live = group < p.n;
-    const uint32_t rec = live ? (p.order ? p.order[group] : group + p.rec_base) : 0u;
+    const bool in_batch = group < p.n;
+    const uint32_t rec = in_batch ? (p.order ? p.order[group] : group + p.rec_base) : 0u;
+    // a record the sequence-parallel path claimed (segments.hip) is not this kernel's -- except
+    // that an open whose tag failed there is zeroed here (the launch boundary orders these zero
+    // stores after every tile's plaintext stores; no plaintext of a failed record is released)
+    const bool claimed = COOP == 0 && in_batch && p.skip && p.skip[rec];
+    if (MODE == MODE_OPEN && claimed && p.ok[rec] == 0) {
+        const uint64_t a = p.out_off[rec], L = p.in_off[rec + 1] - p.in_off[rec];
+        const uint32_t j0 = (blockIdx.x * WGS + threadIdx.x) & (P - 1);
+        for (uint64_t b = 16ull * j0; b < L; b += 16ull * P) {
+            const uint32_t nbytes = (uint32_t)min<uint64_t>(16, L - b);
+            if (nbytes == 16) *reinterpret_cast<uint4*>(p.out + a + b) = make_uint4(0u, 0u, 0u, 0u);
+            else for (uint32_t t = 0; t < nbytes; ++t) p.out[a + b + t] = 0;
+        }
+    }
+    const bool live = in_batch && !claimed;
 
     // ---- record geometry
     uint64_t ioff = 0, ooff = 0, Lin = 0, Lout = 0;

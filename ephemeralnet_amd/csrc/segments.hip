@@ -1,0 +1,430 @@
+// segments.hip -- the sequence-parallel axis: records too long for the record
+// engine's at most 16 lanes are cut into 64 KiB TILES spread over every CU of the chip.
+//
+// Reference shapes this serves: a stored file is ONE chunk of up to 32 MiB
+// (include/ephemeralnet/Config.hpp:62, src/main.cpp:4467, encrypted whole in
+// src/core/Node.cpp:1414-1417 and decrypted whole in Node.cpp:1644-1655); session payloads go up
+// to 1 MiB (src/network/SessionManager.cpp:87).  On the record engine one such record got 16
+// lanes: a lone 32 MiB AEAD record was 32 768 serial ChaCha20 blocks per lane.
+//
+// Three steps on the caller's stream:
+//   1. seg_plan_kernel: every record >= the threshold CLAIMS a contiguous range of tile indices
+//      (one 64-bit CAS on a packed count|tiles word, so entries come out sorted by tile base) and
+//      writes its entry -- for the AEAD also the one-time Poly1305 key and the power table
+//      r^(2^k), k = 0..nbits -- and a claimed[] byte per record that the record engine skips.
+//   2. seg_kernel: a grid of 256-lane workgroups walks the tiles.  Lane j of a tile owns the four
+//      ChaCha20 blocks [tile*1024 + 4j, +4) of its record; a tile whose 64 KiB are all whole blocks
+//      moves them through a wave-private LDS slab with whole 128-byte lines per load / store
+//      instruction (the staging of records_body.hpp COOP 1), a ragged last tile goes per lane.
+//      XOR mode ends there (counter = start + block index, mod 2^32 as ChaCha20.cpp:110).
+//   3. AEAD: lane j's Poly1305 Horner covers its own blocks; the lane scales its accumulator by
+//      r^(tile end - lane end) from the entry's power table and the workgroup sums the lanes: the
+//      tile's partial, normalised at the tile's end.  The last tile of a record to finish (an
+//      agent-scope arrival counter) combines the record's partials -- Horner over whole tiles in
+//      r^4096, one table-power scale per lane -- adds the pad s and writes the tag (seal) or the
+//      verdict (open; a failed record's plaintext is zeroed by that workgroup).
+// No MFMA: nothing here is a contraction.
+#include "enet_device.hpp"
+#include "enet_internal.hpp"
+#include "records_body.hpp"
+
+namespace enet {
+
+namespace {
+
+constexpr uint32_t kSegThreads = 256;                 // lanes per tile workgroup
+constexpr uint32_t kSegBPL = 4;                       // ChaCha20 blocks per lane
+constexpr uint32_t kTileBlocks = kSegThreads * kSegBPL;  // 1024 blocks = 64 KiB
+constexpr uint64_t kTileBytes = 64ull * kTileBlocks;
+constexpr uint32_t kTilePoly = 4 * kTileBlocks;       // Poly1305 blocks per whole tile (4096)
+constexpr int kTileCountBits = 40;                    // header word: count << 40 | tiles
+constexpr unsigned long long kTileMask = (1ull << kTileCountBits) - 1;
+
+}  // namespace
+
+__device__ __forceinline__ void pcarry(uint32_t l[5]) {
+    uint32_t c;
+    c = l[0] >> 26; l[0] &= M26; l[1] += c;
+    c = l[1] >> 26; l[1] &= M26; l[2] += c;
+    c = l[2] >> 26; l[2] &= M26; l[3] += c;
+    c = l[3] >> 26; l[3] &= M26; l[4] += c;
+    c = l[4] >> 26; l[4] &= M26; l[0] += 5u * c;
+    c = l[0] >> 26; l[0] &= M26; l[1] += c;
+}
+
+// l <- l * r^e with the table pw[k] = r^(2^k) (e < 2^nbits)
+__device__ __forceinline__ void pscale(uint32_t l[5], uint32_t e, const uint32_t* pw, uint32_t nbits) {
+    for (uint32_t k = 0; k < nbits; ++k) {
+        if ((e >> k) & 1u) {
+            uint32_t m[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) m[i] = pw[5 * k + i];
+            pmul(l, pmul_make(m));
+        }
+    }
+}
+
+// Sum of the workgroup's 256 accumulators (limbs < 2^27) into thread 0's l (limbs < 2^27)
+__device__ __forceinline__ void wg_sum(uint32_t l[5], uint32_t* red /* [4][5] shared */) {
+#pragma unroll
+    for (int off = 1; off <= 8; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) red[5 * w + i] = l[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i];
+        pcarry(l);
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t seg_counter(const SegParams& p, uint32_t rec) {
+    if (p.mode != MODE_XOR) return 1u;  // RFC 8439 data counter
+    return p.counters ? p.counters[(size_t)rec * (p.counter_stride ? p.counter_stride : 1u)] : 0u;
+}
+
+// ---------------------------------------------------------------------------------- plan
+// Thread per record (grid-stride).  A lone workgroup initialises the header itself; larger grids
+// get it zeroed by the host (hipMemsetAsync) first.
+__global__ __launch_bounds__(kSegThreads) void seg_plan_kernel(SegParams p) {
+    if (gridDim.x == 1) {
+        if (threadIdx.x == 0) __hip_atomic_store(p.hdr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+    for (uint32_t i = blockIdx.x * kSegThreads + threadIdx.x; i < p.n; i += gridDim.x * kSegThreads) {
+        const uint64_t L = p.in_off[i + 1] - p.in_off[i];
+        bool claim = L >= p.long_min && L < kSegMaxLen;
+        uint32_t idx = 0, base = 0;
+        const uint64_t tiles = L ? (L + kTileBytes - 1) / kTileBytes : 1;
+        if (claim) {
+            unsigned long long old = __hip_atomic_load(p.hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (;;) {
+                const uint64_t cnt = old >> kTileCountBits, tb = old & kTileMask;
+                if (cnt >= p.entry_cap || tb + tiles > p.tile_cap) {
+                    claim = false;  // over the scratch the host sized from its hints: record engine
+                    break;
+                }
+                const unsigned long long nw = old + (1ull << kTileCountBits) + tiles;
+                if (__hip_atomic_compare_exchange_strong(p.hdr, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    idx = (uint32_t)cnt;
+                    base = (uint32_t)tb;
+                    break;
+                }
+            }
+        }
+        if (p.claimed) p.claimed[i] = claim ? 1 : 0;
+        if (!claim) continue;
+        SegEntry& e = p.entries[idx];
+        e.rec = i;
+        e.tile_base = base;
+        e.ntiles = (uint32_t)tiles;
+        e.arrived = 0;
+        if (p.mode == MODE_XOR) continue;
+        // AEAD: one-time key = block 0 (RFC 8439 2.6), AAD length, power table
+        uint32_t kw[8], nw[3];
+        const uint32_t* kp = reinterpret_cast<const uint32_t*>(p.keys + (size_t)p.key_stride * i);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) kw[t] = kp[t];
+        const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * i);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) nw[t] = np[t];
+        ChachaRecord R;
+        chacha_record_init(R, kw, nw);
+        uint32_t otk[16];
+        chacha_block(R, 0u, otk);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            e.r[t] = otk[t];
+            e.s[t] = otk[4 + t];
+        }
+        uint32_t aad_len = 0;
+        if (p.aad) aad_len = (uint32_t)(p.aad_off[i + 1] - p.aad_off[i]);
+        e.aad_len = aad_len;
+        const uint64_t K = (uint64_t)((aad_len + 15) >> 4) + (L + 15) / 16 + 1;  // Poly1305 blocks
+        const uint32_t nbits = 64u - (uint32_t)__builtin_clzll(K);
+        e.nbits = nbits;
+        uint32_t x[5];
+        pclamp(x, otk[0], otk[1], otk[2], otk[3]);
+        for (uint32_t k = 0; k < nbits; ++k) {
+#pragma unroll
+            for (int t = 0; t < 5; ++t) e.pw[5 * k + t] = x[t];
+            pmul(x, pmul_make(x));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------- tiles
+template <int MODE>
+__global__ __launch_bounds__(kSegThreads) void seg_kernel(SegParams p) {
+    constexpr bool kPoly = MODE != MODE_XOR;
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kSegThreads * kRun];
+    __shared__ uint32_t red[20];
+    __shared__ uint32_t last_flag;
+    const unsigned long long hw = *p.hdr;
+    const uint32_t count = (uint32_t)(hw >> kTileCountBits);
+    const uint32_t total = (uint32_t)(hw & kTileMask);
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    const uint32_t j = threadIdx.x;
+
+    for (uint32_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+        // the entry whose tile range holds this tile (entries are sorted by tile_base)
+        uint32_t lo = 0, hi = count;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (p.entries[mid].tile_base <= tile) lo = mid;
+            else hi = mid;
+        }
+        SegEntry& E = p.entries[lo];
+        const uint32_t rec = E.rec;
+        const uint32_t tr = tile - E.tile_base;
+        const uint64_t ioff = p.in_off[rec];
+        const uint64_t L = p.in_off[rec + 1] - ioff;
+        const uint64_t ooff = p.out_off[rec];
+        const uint32_t nb = (uint32_t)((L + 63) >> 6);
+        const uint32_t tb0 = tr * kTileBlocks;
+        const uint32_t tb1 = min(tb0 + kTileBlocks, nb);
+        const uint32_t c0 = min(tb0 + kSegBPL * j, tb1), c1 = min(c0 + kSegBPL, tb1);
+        const uint8_t* src = p.in + ioff;
+        uint8_t* dst = p.out + ooff;
+
+        uint32_t kw[8], nw[3];
+        {
+            const uint32_t* kp = reinterpret_cast<const uint32_t*>(p.keys + (size_t)p.key_stride * rec);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kw[i] = kp[i];
+            const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * rec);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) nw[i] = np[i];
+        }
+        ChachaRecord R;
+        chacha_record_init(R, kw, nw);
+        const uint32_t ctr0 = seg_counter(p, rec);
+
+        // Poly1305 state: lane 0 of the record's first tile absorbs the AAD prefix
+        uint32_t h[5] = {0, 0, 0, 0, 0};
+        PolyR32 PR{};
+        uint32_t na = 0, aad_len = 0;
+        const uint32_t nct = (uint32_t)((L + 15) >> 4);
+        if (kPoly) {
+            PR = polyr32_make(E.r[0], E.r[1], E.r[2], E.r[3]);
+            aad_len = E.aad_len;
+            na = (aad_len + 15) >> 4;
+            if (tr == 0 && j == 0 && na) {
+                const uint8_t* ap = p.aad + p.aad_off[rec];
+                for (uint32_t s = 0; s < na; ++s) {
+                    const uint32_t cnt = min(16u, aad_len - 16u * s);
+                    uint32_t w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if ((uint32_t)(4 * i + b) < cnt) v |= (uint32_t)ap[16 * s + 4 * i + b] << (8 * b);
+                        w[i] = v;
+                    }
+                    poly32_block(h, PR, w[0], w[1], w[2], w[3], 1u);
+                }
+            }
+        }
+
+        const bool whole = (uint64_t)(tb0 + kTileBlocks) * 64ull <= L;  // uniform over the workgroup
+        if (whole) {
+            // two stages of two blocks per lane; load / store instruction i serves the owners
+            // 8i .. 8i+7 of the wave, eight lanes per owner = one whole 128-byte run each
+            const uint32_t kk = lane & 7u;
+            const uint32_t msw = slab_sw(lane);
+            uint8_t* wslab = slab + wbase * kRun;
+            uint8_t* myrun = slab + threadIdx.x * kRun;
+            const uint8_t* ib = src + 64ull * tb0;
+            uint8_t* ob = dst + 64ull * tb0;
+            const bool nt = ((reinterpret_cast<uintptr_t>(ob)) & 63u) == 0;
+            uint32_t offs[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t o = 8u * i + (lane >> 3);
+                offs[i] = 64u * kSegBPL * (wbase + o) + 16u * (kk ^ slab_sw(o));
+            }
+            uint32_t pf[32];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(ib + offs[i]);
+                pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) =
+                        make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+                ENET_WAVE_LDS_SYNC();
+                uint32_t w2[32];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                    w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
+                }
+                if (st == 0) {  // the second stage's lines fly under this stage's rounds
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint4 v = *reinterpret_cast<const uint4*>(ib + offs[i] + kRun);
+                        pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                    }
+                    asm volatile("" : "+v"(R.k[0])::"memory");
+                }
+                const uint32_t cb = ctr0 + c0 + 2u * st;  // u32 wrap (ChaCha20.cpp:110)
+                if (MODE == MODE_OPEN) {
+                    poly_block64(h, PR, w2);
+                    poly_block64(h, PR, w2 + 16);
+                }
+                uint32_t ka[16], kb[16];
+                chacha_block2(R, cb, cb + 1u, ka, kb);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+                if (MODE == MODE_SEAL) {
+                    poly_block64(h, PR, w2);
+                    poly_block64(h, PR, w2 + 16);
+                }
+                ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                        make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+                ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                    store_stream(ob + offs[i] + kRun * st, v, nt);
+                }
+            }
+        } else {
+            // the record's ragged last tile: per lane, partial block masked
+            for (uint32_t c = c0; c < c1; ++c) {
+                const uint64_t pos = 64ull * c;
+                const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
+                uint32_t w[16];
+                load_block(src + pos, nbytes, w, pos + nbytes >= 16);
+                uint32_t o[16];
+                chacha_block(R, ctr0 + c, o);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) o[i] ^= w[i];
+                store_block(dst + pos, nbytes, o);
+                if (kPoly) {
+                    uint32_t* ct = (MODE == MODE_SEAL) ? o : w;
+                    if (MODE == MODE_SEAL && nbytes < 64) mask_tail(ct, nbytes);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (4 * c + u < nct)
+                            poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
+                }
+            }
+        }
+
+        if (kPoly) {
+            // the lane holding the record's last block absorbs the length block
+            const bool last_tile = tb1 == nb;
+            const bool has_last = (c1 == nb && c1 > c0) || (nb == 0 && j == 0);
+            if (has_last) poly32_block(h, PR, aad_len, 0u, (uint32_t)L, (uint32_t)(L >> 32), 1u);
+            // positions (Poly1305 block index + 1) where this lane's and the tile's runs end
+            const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
+            const uint32_t tile_end = na + min(4u * tb1, nct) + (last_tile ? 1u : 0u);
+            uint32_t l[5];
+            h32_to_limbs(h, l);
+            if (c1 > c0 || (tr == 0 && j == 0)) pscale(l, tile_end - lane_end, E.pw, min(E.nbits, 14u));
+            wg_sum(l, red);
+            // Publish the tile's partial; the record's last tile to arrive finishes the record.
+            // Hand-off without an L2 write-back (MI355X_MICROARCH.md, inter-workgroup visibility,
+            // first row of the sc1 table): thread 0 stores the partial write-through (sc1),
+            // drains it (vmcnt 0), then takes a ticket with a relaxed agent-scope add; the
+            // workgroup whose add comes last reads every partial with sc1 loads after a barrier.
+            // (__threadfence() here wrote back the XCD's whole L2 once per tile.)
+            uint32_t* part = p.partials + 8ull * tile;
+            if (threadIdx.x == 0) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) __hip_atomic_store(part + i, l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t prev = __hip_atomic_fetch_add(&E.arrived, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last_flag = prev + 1 == E.ntiles ? 1u : 0u;
+            }
+            __syncthreads();
+            if (last_flag) {
+                const uint32_t nt = E.ntiles;
+                const uint32_t K = na + nct + 1;
+                // whole tiles [0, nt-1) end at na + 4096 (t+1); the last one at K.  Lane j runs
+                // Horner in r^4096 over its contiguous tiles, then scales by r^(K - its end).
+                const uint32_t nw = nt - 1;
+                const uint32_t q = (nw + kSegThreads - 1) / kSegThreads;
+                const uint32_t t0 = min(j * q, nw), t1 = min(t0 + q, nw);
+                uint32_t acc[5] = {0, 0, 0, 0, 0};
+                auto load_part = [&](uint32_t t) {
+                    const uint32_t* v = p.partials + 8ull * (E.tile_base + t);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) acc[i] += __hip_atomic_load(v + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    pcarry(acc);
+                };
+                if (t1 > t0) {
+                    uint32_t m4096[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) m4096[i] = E.pw[5 * 12 + i];
+                    const Pmul M = pmul_make(m4096);
+                    for (uint32_t t = t0; t < t1; ++t) {
+                        if (t > t0) pmul(acc, M);
+                        load_part(t);
+                    }
+                    pscale(acc, K - (na + kTilePoly * t1), E.pw, E.nbits);
+                }
+                if (j == kSegThreads - 1) load_part(nt - 1);  // already normalised at K
+                wg_sum(acc, red);
+                if (threadIdx.x == 0) {
+                    uint32_t tag[4];
+                    pfinish(acc, E.s, tag);
+                    if (MODE == MODE_SEAL) {
+                        uint32_t* tp = reinterpret_cast<uint32_t*>(p.tag_out + 16ull * rec);
+                        tp[0] = tag[0]; tp[1] = tag[1]; tp[2] = tag[2]; tp[3] = tag[3];
+                    } else {
+                        // a failed record's plaintext is zeroed by the record kernel launched
+                        // after this one (records_body: claimed records with ok == 0): zero
+                        // stores from here could be overtaken by other tiles' plaintext still
+                        // dirty in their XCD's L2
+                        const uint32_t* tp = reinterpret_cast<const uint32_t*>(p.tag_in + 16ull * rec);
+                        const uint32_t diff = (tag[0] ^ tp[0]) | (tag[1] ^ tp[1]) | (tag[2] ^ tp[2]) | (tag[3] ^ tp[3]);
+                        p.ok[rec] = diff == 0 ? 1 : 0;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the slab and red[] are reused by the next tile
+    }
+}
+
+// ---------------------------------------------------------------------------------- host side
+hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_blocks, hipStream_t s) {
+    if (plan_blocks > 1) {
+        if (hipError_t e = hipMemsetAsync(p.hdr, 0, sizeof(unsigned long long), s)) return e;
+    }
+    hipLaunchKernelGGL(seg_plan_kernel, dim3(plan_blocks), dim3(kSegThreads), 0, s, p);
+    switch (p.mode) {
+        case MODE_XOR: hipLaunchKernelGGL(seg_kernel<MODE_XOR>, dim3(tile_blocks), dim3(kSegThreads), 0, s, p); break;
+        case MODE_SEAL: hipLaunchKernelGGL(seg_kernel<MODE_SEAL>, dim3(tile_blocks), dim3(kSegThreads), 0, s, p); break;
+        case MODE_OPEN: hipLaunchKernelGGL(seg_kernel<MODE_OPEN>, dim3(tile_blocks), dim3(kSegThreads), 0, s, p); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace enet

@@ -10,8 +10,12 @@
  * Conventions
  *   - All buffer pointers are DEVICE pointers (hipMalloc'd, or any device-accessible memory)
  *     unless a comment says otherwise.  `stream` is a hipStream_t (NULL = legacy default).
- *   - Calls are asynchronous on `stream`; nothing is allocated, freed or synchronised inside
- *     them (safe to capture in a hipGraph).  The caller keeps ownership of every buffer.
+ *   - Calls are asynchronous on `stream`; nothing is synchronised inside them (safe to capture in
+ *     a hipGraph).  The caller keeps ownership of every buffer.  The one allocation: batches
+ *     holding records of >= 256 KiB (ENET_SEG_MIN; enet_set_seg_min) take the sequence-parallel
+ *     path, whose small scratch (a header, one entry per long record, one byte per record, 32 B
+ *     per 64 KiB tile) is stream-ordered memory from a library-private pool
+ *     (hipMallocFromPoolAsync / hipFreeAsync on `stream`).
  *   - Records are described SoA: a byte arena plus uint64 offsets[n+1]; record i is
  *     arena[offsets[i] .. offsets[i+1]).  Input and output arenas have their own offsets so
  *     length-changing ops (frames: +32-byte MAC) and in-place ops (out == in) both work.
@@ -360,6 +364,17 @@ ENET_API uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, ui
 /* Force lanes per record (1, 2, 4, 8 or 16) for all later calls in this process; 0 restores the
  * scheduler.  Returns ENET_EINVAL for other values.  Tuning / test knob. */
 ENET_API int enet_set_lanes_per_record(uint32_t lanes);
+/* Sequence-parallel path (segments.hip) for enet_chacha20_xor_batch / enet_aead_seal_batch /
+ * enet_aead_open_batch: a record of >= ENET_SEG_MIN bytes is cut into 64 KiB tiles spread over
+ * every CU, the tiles' Poly1305 partials combined on the device (a lone 32 MiB record otherwise
+ * gets 16 lanes).  Automatic (-1, default) when max_len_hint >= ENET_SEG_MIN, unless the batch is
+ * uniform with count * 16 >= 131072 lanes (the record kernels fill the chip then); a value >= 0
+ * sends every record of at least that many bytes to the tiles whatever the hints (0: every
+ * record; INT64_MAX: never).  Results are identical; tuning / test knob. */
+#define ENET_SEG_MIN (256u << 10)
+ENET_API int enet_set_seg_min(int64_t bytes);
+/* Batches that have taken the sequence-parallel path in this process (tests / tuning). */
+ENET_API uint64_t enet_seg_batches(void);
 /* Staging of uniform-length batches (all records the same length): 1 = register prefetch + LDS
  * transposition (default; records that are not 128-byte aligned and get one lane each are staged
  * as whole aligned 128-byte lines), 4 = 1 without the line staging, 3 = LDS DMA with one live

@@ -17,6 +17,9 @@
 #              (oracle/_ref/scalar_latency_gpu: median of 200 calls, then 16 threads)
 #   seal       host engine frame seal: stitched vs two-pass by size (tools/seal_variants,
 #              tools/seal_bench), then the blocking host-engine queue rows (1 and 16 threads)
+#   sessions   the reference's thread-per-session load (SessionManager.cpp:331-332, 337-388, 822):
+#              T session threads, each with ONE blocking frame in flight (queue_bench sync), device
+#              queue vs host engine vs auto, T = ${THREADS:-64 256 768}, two rounds
 # Round-wide evidence (kernel stats, PMC, side configs): tools/gpu_round.sh.
 set -euo pipefail
 R=${1:?recipe}
@@ -141,6 +144,12 @@ seal)
   done; done
   cat $O/cpu.txt $O/seal_variants.jsonl $O/seal_bench.jsonl
   qsummary $O/host_queue.jsonl ;;
+sessions)
+  CPUS=$(node_cpus); : > $O/sessions.jsonl
+  for r in 1 2; do for t in ${THREADS:-64 256 768}; do for pol in ${POLICIES:-device host auto}; do
+    QUEUE_BENCH_WARMUP=${WARMUP:-0.3} timeout -k 10 90 taskset -c $CPUS tools/queue_bench $pol sync $t 1 1.0 >> $O/sessions.jsonl 2>> $O/sessions.err
+  done; done; done
+  qsummary $O/sessions.jsonl ;;
 *)
   echo "unknown recipe $R" >&2; exit 2 ;;
 esac
