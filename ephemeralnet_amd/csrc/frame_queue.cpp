@@ -125,7 +125,15 @@ inline void prof_add(int i, std::uint64_t& t0) {
     t_prof.n[i] += 1;
     t0 = t;
 }
+// ENET_QUEUE_STALL_OVERFLOW_US=<us> (tools build only): a submitter whose reservation found its
+// pass full sleeps that long before closing it -- the preemption window of ADVICE r05's stale
+// close, made wide for tests/cpp/queue_stress
+void stall_overflow() {
+    static const int us = std::getenv("ENET_QUEUE_STALL_OVERFLOW_US") ? std::atoi(std::getenv("ENET_QUEUE_STALL_OVERFLOW_US")) : 0;
+    if (us > 0) std::this_thread::sleep_for(std::chrono::microseconds(us));
+}
 #else
+inline void stall_overflow() {}
 constexpr double fake_us() { return 0.0; }
 inline std::uint64_t prof_t() { return 0; }
 inline void prof_add(int, std::uint64_t&) {}
@@ -307,7 +315,10 @@ struct FrameTicket::State {
     std::uint32_t idx = 0;
     std::uint64_t gen = 0;
     bool viewing = false;  // the slot is kViewing: this ticket holds a view into the pass
-    bool counted = false;  // counted in its submitting thread's backlog (t_backlog)
+    // AUTO's routing signals this ticket is counted in until it is collected or dropped (on
+    // whatever thread): its submitting thread's backlog, and its shard of the process-wide count
+    std::shared_ptr<std::atomic<std::int32_t>> backlog;
+    std::atomic<std::int64_t>* inflight = nullptr;
     std::optional<std::vector<std::uint8_t>> result;
 };
 
@@ -362,7 +373,9 @@ struct Pass {
     alignas(64) std::atomic<std::uint64_t> res{kClosedBit};
     alignas(64) std::atomic<std::int64_t> first_us{0};
     std::atomic<int> state{kDone};
-    std::uint64_t gen = 0;       // generation: +1 each time the pass is reopened
+    // generation: +1 each time the pass is reopened (under the queue's mu_; read without it by a
+    // submitter, before its reservation, to tie a later close_full to that generation)
+    std::atomic<std::uint64_t> gen{0};
     std::uint32_t reserved = 0;  // reservations made before the close (some may be overflows)
     std::uint32_t n = 0;         // final slot count (set when the pass runs)
     std::uint32_t rel_scan = 0;  // released(): slots [0, rel_scan) are known released (under mu_)
@@ -425,9 +438,34 @@ struct StateCache {
     std::vector<FrameTicket::State*> v;
     ~StateCache();
 };
-// This thread's submitted, uncollected tickets (any route; decremented by the collecting thread,
-// clamped at 0): the backlog signal of the AUTO policy (use_queue_async)
-thread_local std::int32_t t_backlog = 0;
+// The AUTO policy's signals (use_queue_async), counted for every non-blocking submission whatever
+// its route and uncounted when its ticket is collected or dropped, on any thread:
+//  * the submitting thread's backlog -- a counter the thread shares with its tickets, so a ticket
+//    collected by another thread (a reader thread submits, a writer thread collects) or after the
+//    submitter exited decrements the right one (a thread-local count only grew on the
+//    submitting side of such a split, sending trickle loads to the device);
+//  * the process-wide count per direction (many session threads, each with a
+//    few frames in flight), sharded over cache lines by thread so submitters do not share one.
+struct ThreadBacklog {
+    std::shared_ptr<std::atomic<std::int32_t>> c = std::make_shared<std::atomic<std::int32_t>>(0);
+};
+thread_local ThreadBacklog t_backlog;
+struct alignas(64) PaddedCount {
+    std::atomic<std::int64_t> v{0};
+};
+constexpr unsigned kCountShards = 16;
+PaddedCount g_inflight[2][kCountShards];
+std::atomic<unsigned> g_next_count_shard{0};
+std::atomic<std::int64_t>* inflight_slot(bool open_dir) {
+    thread_local const unsigned sh = g_next_count_shard.fetch_add(1, std::memory_order_relaxed) % kCountShards;
+    return &g_inflight[open_dir ? 1 : 0][sh].v;
+}
+void count_submission(FrameTicket::State* s, bool open_dir) {
+    s->backlog = t_backlog.c;
+    s->backlog->fetch_add(1, std::memory_order_relaxed);
+    s->inflight = inflight_slot(open_dir);
+    s->inflight->fetch_add(1, std::memory_order_relaxed);
+}
 thread_local int t_cache_state = 0;  // 0 untouched, 1 live, 2 destroyed (trivially destructible)
 thread_local StateCache t_cache;
 StateCache::~StateCache() {
@@ -446,8 +484,14 @@ FrameTicket::State* new_state() {
     return x;
 }
 void free_state(FrameTicket::State* x) {
-    if (x->counted && t_backlog > 0) --t_backlog;
-    x->counted = false;
+    if (x->backlog) {
+        x->backlog->fetch_sub(1, std::memory_order_relaxed);
+        x->backlog.reset();
+    }
+    if (x->inflight) {
+        x->inflight->fetch_sub(1, std::memory_order_relaxed);
+        x->inflight = nullptr;
+    }
     x->result.reset();
     x->viewing = false;
     x->st.store(kHasResult, std::memory_order_relaxed);
@@ -610,10 +654,14 @@ public:
         const std::uint64_t len = in.size();
         Shard& sh = shards_[my_shard(plan_)];
         std::uint64_t pt = prof_t();
+        // the nonce is drawn before any slot is reserved: NonceSource::refill may throw
+        // (std::random_device), and a reserved slot never filled would stall its pass's worker
+        // in spin_until forever
+        std::uint8_t nonce[12];
+        if (!open_dir_) nonce_source().draw(nonce);
         auto* ts = new_state();
         ts->st.store(kInPass, std::memory_order_relaxed);
-        ts->counted = true;
-        ++t_backlog;
+        count_submission(ts, open_dir_);
         prof_add(0, pt);
         for (;;) {
             Pass* p = sh.open.load(std::memory_order_acquire);
@@ -623,6 +671,9 @@ public:
                 prof_add(8, pt);
                 continue;
             }
+            // the generation this reservation lands in, or an older one (then close_full below
+            // leaves the pass alone; the retry reads the current one)
+            const std::uint64_t g0 = p->gen.load(std::memory_order_acquire);
             const std::uint64_t v = p->res.fetch_add((1ull << kSlotShift) | len, std::memory_order_acq_rel);
             if (v & kClosedBit) {  // taken by a worker: the shard's next open pass
                 prof_add(1, pt);
@@ -635,16 +686,18 @@ public:
             if (idx >= p->cap_frames || used + len > p->cap_in) {
                 // full: this and every later reservation of the pass is past its end; the first
                 // one marks the cut (a slot index below capacity), whoever closes it runs it
-                if (idx < p->cap_frames) p->recs[idx].fill.store(p->gen << 2 | kOverflow, std::memory_order_release);
+                if (idx < p->cap_frames)  // the pass cannot run before this mark: its generation is still ours
+                    p->recs[idx].fill.store(p->gen.load(std::memory_order_relaxed) << 2 | kOverflow, std::memory_order_release);
                 overflows_.fetch_add(1, std::memory_order_relaxed);
                 prof_add(1, pt);
-                close_full(sh, p);
+                stall_overflow();
+                close_full(p, g0);
                 prof_add(9, pt);
                 continue;
             }
             if (idx == 0) p->first_us.store((std::int64_t)now_us(), std::memory_order_relaxed);
             prof_add(1, pt);
-            fill_slot(*p, idx, used, key, in, ts);
+            fill_slot(*p, idx, used, key, nonce, in, ts);
             prof_add(2, pt);
             if (idx == 0 || idx + 1 == target_frames_ || (used < target_bytes_ && used + len >= target_bytes_)) {
                 std::lock_guard<std::mutex> lk(mu_);  // no lost wake-up: workers check under mu_
@@ -680,14 +733,14 @@ private:
     };
 
     void fill_slot(Pass& p, std::uint32_t idx, std::uint64_t at, const std::uint8_t key[32],
-                   std::span<const std::uint8_t> in, FrameTicket::State* ts) {
+                   const std::uint8_t nonce[12], std::span<const std::uint8_t> in, FrameTicket::State* ts) {
         SlotRec& r = p.recs[idx];  // this slot's own cache lines
-        const std::uint64_t gen = p.gen;  // stable: the pass cannot run before this slot is filled
+        const std::uint64_t gen = p.gen.load(std::memory_order_relaxed);  // stable: the pass cannot run before this slot is filled
         r.in_at = at;
         r.len = in.size();
         r.ticket = ts;
         std::memcpy(r.key, key, 32);
-        if (!open_dir_) nonce_source().draw(r.nonce);
+        if (!open_dir_) std::memcpy(r.nonce, nonce, 12);
         if (!in.empty()) enet::hb::copy_streaming(p.h + p.o_in + at, in.data(), in.size());
         _mm_sfence();  // the streamed lines are visible before the fill word says so
         ts->pass = &p;
@@ -750,7 +803,8 @@ private:
         if (p.state.load(std::memory_order_acquire) != kDone) return false;
         for (; p.rel_scan < p.n; ++p.rel_scan) {
             const std::uint64_t v = p.recs[p.rel_scan].tk.load(std::memory_order_acquire);
-            if (v != (p.gen << 3 | kReleased) && v != (p.gen << 3 | kEvicted)) return false;
+            const std::uint64_t g = p.gen.load(std::memory_order_relaxed);
+            if (v != (g << 3 | kReleased) && v != (g << 3 | kEvicted)) return false;
         }
         return true;
     }
@@ -760,7 +814,7 @@ private:
     // be reused until that ticket releases it
     std::uint64_t evict(Pass& p, bool* complete = nullptr) {
         std::uint64_t moved = 0;
-        const std::uint64_t g = p.gen << 3;
+        const std::uint64_t g = p.gen.load(std::memory_order_relaxed) << 3;
         if (complete) *complete = true;
         for (std::uint32_t i = 0; i < p.n; ++i) {
             SlotRec& r = p.recs[i];
@@ -788,7 +842,7 @@ private:
     // Make p the shard's open pass (its old tickets all released or evicted)
     // O(1): the new generation retires every slot word of the old one
     void reopen(Shard& sh, Pass& p) {
-        p.gen += 1;
+        p.gen.store(p.gen.load(std::memory_order_relaxed) + 1, std::memory_order_release);
         p.n = 0;
         p.rel_scan = 0;
         p.reserved = 0;
@@ -891,10 +945,17 @@ private:
         return true;
     }
 
-    void close_full(Shard& sh, Pass* p) {
-        std::lock_guard<std::mutex> lk(mu_);
+    // Close a pass a reservation found full.  Only the generation that reservation was made in:
+    // a submitter delayed between its reservation and this call may find the pass closed, run,
+    // released and reopened -- for another shard, too -- and closing that generation would leave
+    // the new owner's open pointer on a closed pass that no worker takes and no submitter
+    // reopens.  Once closed, no shard keeps it as its open pass.
+    void close_full(Pass* p, std::uint64_t gen) {
+        std::lock_guard<std::mutex> lk(mu_);  // reopen() runs under mu_: gen is stable here
+        if (p->gen.load(std::memory_order_relaxed) != gen) return;
         if (close_pass(*p)) {
-            if (sh.open.load(std::memory_order_relaxed) == p) sh.open.store(nullptr, std::memory_order_release);
+            for (auto& s : shards_)
+                if (s.open.load(std::memory_order_relaxed) == p) s.open.store(nullptr, std::memory_order_release);
             closed_.push_back(p);
             work_cv_.notify_one();
         }
@@ -1034,7 +1095,7 @@ private:
         const std::uint32_t lim = std::min(p.reserved, p.cap_frames);
         std::uint32_t n = lim;
         for (std::uint32_t i = 0; i < lim; ++i)
-            if (spin_until(p.recs[i].fill, p.gen) == kOverflow) {
+            if (spin_until(p.recs[i].fill, p.gen.load(std::memory_order_relaxed)) == kOverflow) {
                 n = i;
                 break;
             }
@@ -1157,24 +1218,32 @@ private:
     double dev_passes_ = 0, sum_pass_us_ = 0, sum_kernel_us_ = 0, sum_fill_us_ = 0;
 };
 
-// a ticket whose result is known on the caller's thread
-FrameTicket ready_ticket(std::optional<std::vector<std::uint8_t>> r) {
+// a ticket whose result is known on the caller's thread (counted like a queued one: AUTO's signals
+// see every non-blocking submission, whichever route served it)
+FrameTicket ready_ticket(std::optional<std::vector<std::uint8_t>> r, bool open_dir, bool counted = true) {
     auto* s = new_state();
     s->result = std::move(r);
-    s->counted = true;
-    ++t_backlog;
+    if (counted) count_submission(s, open_dir);
     return FrameTicket(s);
 }
 
-// Non-blocking submissions: the queue under DEVICE; under AUTO when the device is there and the
-// submitting thread keeps a backlog of >= 320 uncollected frames -- where the device queue
-// overtakes the host engine in frames/s (box, 1 500-byte frames, 16 threads, sealed / opened
-// M frames/s device vs the stitched host engine: x 256 in flight 10.9-11.0 / 11.7-11.8 vs
-// 13.2-13.3 / 11.9-12.6, x 384 12.6-12.8 / 13.0 vs 13.2 / 11.9-12.8, x 512 13.4-14.0 / 13.5-13.7
-// vs 11.9-13.1 / 12.8; profiles/r05_seal_crossover_hi.jsonl; below ~64 per thread the device is
-// 5-100x slower, profiles/r05s_crossover.jsonl).  The device costs a third of the CPU per frame
-// at every one of these (0.35-0.44 vs 1.2-1.35 us): ENET_SCALAR_DEVICE is the choice for a relay
-// whose cores have other work.  Tools build: ENET_QUEUE_AUTO_BACKLOG overrides.
+// Non-blocking submissions: the queue under DEVICE; under AUTO when the device is there and either
+//  * the submitting thread holds >= 320 uncollected frames -- where the device queue overtakes the
+//    host engine in frames/s for a few deep submitters (box, 1 500-byte frames, 16 threads, sealed /
+//    opened M frames/s device vs the stitched host engine: x 256 in flight 10.9-11.0 / 11.7-11.8 vs
+//    13.2-13.3 / 11.9-12.6, x 384 12.6-12.8 / 13.0 vs 13.2 / 11.9-12.8, x 512 13.4-14.0 / 13.5-13.7
+//    vs 11.9-13.1 / 12.8; profiles/r05_seal_crossover_hi.jsonl; below ~64 per thread the device is
+//    5-100x slower, profiles/r05s_crossover.jsonl), or
+//  * the process holds >= 320 uncollected frames per CPU of its budget in this direction -- many
+//    session threads with a few frames each: the host engine's rate is bounded by the CPUs
+//    (~0.8 M frames/s each), the device queue's by the frames in flight (profiles/
+//    r06_sessions_async.jsonl).
+// Blocking seal() / open() never take the queue under AUTO: one frame per blocked session thread
+// costs a thread wake-up per frame (7-11 us of CPU), and 64-768 blocked threads moved 0.2-2.2 M
+// frames/s through the device queue against 7-10 M on the host engine
+// (profiles/r06_sessions_blocking.jsonl).  The device costs a third of the CPU per frame once it
+// is fed (0.35-0.44 vs 1.2-1.35 us): ENET_SCALAR_DEVICE is the choice for a relay whose cores have
+// other work.  Tools build: ENET_QUEUE_AUTO_BACKLOG overrides the 320.
 std::int32_t auto_backlog() {
     static const std::int32_t v = [] {
         std::int32_t b = 320;
@@ -1185,9 +1254,34 @@ std::int32_t auto_backlog() {
     }();
     return v;
 }
-bool use_queue_async(const Core& c) {
+std::int64_t cpu_budget() {
+    static const std::int64_t v = [] {
+        std::int64_t b = (std::int64_t)enet::topo::allowed_cpus().size();
+        if (const std::uint32_t q = enet::topo::cgroup_quota_cpus()) b = std::min<std::int64_t>(b, q);
+        if (const std::uint32_t e = enet::topo::env_cpus()) b = std::min<std::int64_t>(b, e);
+        return std::max<std::int64_t>(1, b);
+    }();
+    return v;
+}
+// the process-wide count of one direction, re-summed every 16th call on a thread (the shards sit on
+// lines other threads write; one sum is 16 cache-line reads)
+std::int64_t inflight_estimate(bool open_dir) {
+    thread_local std::int64_t cached[2] = {0, 0};
+    thread_local std::uint32_t calls[2] = {0, 0};
+    const int d = open_dir ? 1 : 0;
+    if ((calls[d]++ & 15u) == 0) {
+        std::int64_t sum = 0;
+        for (auto& c : g_inflight[d]) sum += c.v.load(std::memory_order_relaxed);
+        cached[d] = sum;
+    }
+    return cached[d];
+}
+bool use_queue_async(const Core& c, bool open_dir) {
     const int pol = enet::scalar::g_policy.load();
-    return pol == ENET_SCALAR_DEVICE || (pol == ENET_SCALAR_AUTO && c.has_device() && t_backlog >= auto_backlog());
+    if (pol == ENET_SCALAR_DEVICE) return true;
+    if (pol != ENET_SCALAR_AUTO || !c.has_device()) return false;
+    return t_backlog.c->load(std::memory_order_relaxed) >= auto_backlog() ||
+           inflight_estimate(open_dir) >= (std::int64_t)auto_backlog() * cpu_budget();
 }
 
 }  // namespace
@@ -1327,13 +1421,13 @@ std::optional<std::vector<std::uint8_t>> FrameQueue::seal(const std::array<std::
 }
 
 FrameTicket FrameQueue::submit(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message) {
-    if (message.size() + kMac > kMaxPayloadSize) return ready_ticket(std::nullopt);
-    if (!use_queue_async(impl_->core)) {
+    if (message.size() + kMac > kMaxPayloadSize) return ready_ticket(std::nullopt, false, false);
+    if (!use_queue_async(impl_->core, false)) {
         std::uint8_t nonce[12];
         nonce_source().draw(nonce);
         enet::scalar::host_call();
         impl_->core.count_direct();
-        return ready_ticket(host_wire_seal(session_key.data(), nonce, message));
+        return ready_ticket(host_wire_seal(session_key.data(), nonce, message), false);
     }
     return impl_->core.submit(session_key.data(), message);
 }
@@ -1409,13 +1503,13 @@ std::optional<std::vector<std::uint8_t>> FrameReceiveQueue::open(const std::arra
 
 FrameTicket FrameReceiveQueue::submit(const std::array<std::uint8_t, 32>& session_key,
                                       std::span<const std::uint8_t> frame) {
-    if (!frame_shape_ok(frame)) return ready_ticket(std::nullopt);
-    if (!use_queue_async(impl_->core)) {
+    if (!frame_shape_ok(frame)) return ready_ticket(std::nullopt, true, false);
+    if (!use_queue_async(impl_->core, true)) {
         enet::scalar::host_call();
         impl_->core.count_direct();
         std::vector<std::uint8_t> m;
-        if (!host_wire_open(session_key.data(), frame, m)) return ready_ticket(std::nullopt);
-        return ready_ticket(std::move(m));
+        if (!host_wire_open(session_key.data(), frame, m)) return ready_ticket(std::nullopt, true);
+        return ready_ticket(std::move(m), true);
     }
     return impl_->core.submit(session_key.data(), frame);
 }

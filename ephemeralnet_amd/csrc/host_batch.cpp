@@ -1131,6 +1131,7 @@ SharedSet& shared_set(int dev) {
 void run_shared(int dev, const Job& job) {
     SharedSet& set = shared_set(dev);
     size_t idx = 0;
+    Engine* eng = nullptr;  // read under set.mu: another caller may grow set.engines meanwhile
     {
         std::unique_lock<std::mutex> lk(set.mu);
         for (;;) {
@@ -1149,6 +1150,7 @@ void run_shared(int dev, const Job& job) {
             set.cv.wait(lk);
         }
         set.busy[idx] = true;
+        eng = set.engines[idx];
     }
     struct Release {
         SharedSet& set;
@@ -1161,7 +1163,7 @@ void run_shared(int dev, const Job& job) {
             set.cv.notify_one();
         }
     } release{set, idx};
-    set.engines[idx]->run(job);
+    eng->run(job);
 }
 
 Engine* create_engine(int dev, const Config& cfg) { return new Engine(dev, cfg); }

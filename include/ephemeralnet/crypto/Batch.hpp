@@ -240,9 +240,13 @@ public:
                                                   std::span<const std::uint8_t> message);
     // Non-blocking seal: the message is copied into the queue before this returns.
     FrameTicket submit(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> message);
-    // The same as a std::future (deferred: get() / wait() collect the result on the calling
-    // thread; wait_for / wait_until report std::future_status::deferred -- use submit() and
-    // FrameTicket::ready() to poll).
+    // DEPRECATED (ABI 1.2): the same as a std::future with std::launch::deferred -- get() / wait()
+    // collect the result on the calling thread, but wait_for / wait_until return
+    // std::future_status::deferred and never report readiness.  Before ABI 1.2 the future became
+    // ready when its pass had run; a caller that polls futures must move to submit() and
+    // FrameTicket::ready() / view() (a promise per frame cost ~0.45 us of CPU per frame, DESIGN.md
+    // section 6).  Kept for source compatibility of get()-style callers.
+    [[deprecated("poll with submit() + FrameTicket::ready(); the returned future is deferred")]]
     std::future<std::optional<std::vector<std::uint8_t>>> seal_async(const std::array<std::uint8_t, 32>& session_key,
                                                                       std::vector<std::uint8_t> message);
     // Explicit batching (a sender that collects frames itself): push queues a message (false =
@@ -274,6 +278,8 @@ public:
                                                   std::span<const std::uint8_t> frame);
     // Non-blocking open (see FrameQueue::submit / seal_async).
     FrameTicket submit(const std::array<std::uint8_t, 32>& session_key, std::span<const std::uint8_t> frame);
+    // DEPRECATED (ABI 1.2): a deferred future, as FrameQueue::seal_async.
+    [[deprecated("poll with submit() + FrameTicket::ready(); the returned future is deferred")]]
     std::future<std::optional<std::vector<std::uint8_t>>> open_async(const std::array<std::uint8_t, 32>& session_key,
                                                                      std::vector<std::uint8_t> frame);
     FrameQueueStats stats() const;

@@ -12,7 +12,9 @@
 // own messages.  Prints a sample of (key, message, frame) lines for the oracle check in
 // tests/test_frame_queue.py and a summary line.
 #include <algorithm>
+#include <condition_variable>
 #include <deque>
+#include <mutex>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -45,6 +47,19 @@ std::string hex(const std::vector<std::uint8_t>& v) {
         s += d[b & 15];
     }
     return s.empty() ? "-" : s;
+}
+
+// Every sealed frame against the host engine's bytes for the same key, message and nonce (the
+// nonce from the frame's header): header nonce(12) || BE32(|m| + 32), body = the host engine's
+// seal_body (SessionManager.cpp:362-387, Message.cpp:305-311).  The host engine is itself pinned
+// to the oracle (tests/test_host_engine.py).  Returns true when the frame differs.
+bool frame_mismatch(const std::array<std::uint8_t, 32>& key, const std::vector<std::uint8_t>& m,
+                    const std::vector<std::uint8_t>& f) {
+    if (f.size() != m.size() + 48) return true;
+    std::vector<std::uint8_t> body(m.size() + 32);
+    enet_host_seal_body(key.data(), f.data(), m.data(), m.size(), body.data());
+    const std::uint32_t len = (std::uint32_t)f[12] << 24 | (std::uint32_t)f[13] << 16 | (std::uint32_t)f[14] << 8 | f[15];
+    return len != m.size() + 32 || !std::equal(body.begin(), body.end(), f.begin() + 16);
 }
 
 }  // namespace
@@ -84,7 +99,7 @@ int async_mode(const std::string& policy, int T, int F) {
                                                                                       : ENET_SCALAR_AUTO, 0);
     FrameQueue tx;
     FrameReceiveQueue rx;
-    std::atomic<int> bad{0}, opened{0}, rejected{0};
+    std::atomic<int> bad{0}, opened{0}, rejected{0}, mismatch{0};
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
         th.emplace_back([&, t] {
@@ -102,6 +117,7 @@ int async_mode(const std::string& policy, int T, int F) {
             for (int i = 0; i < F; ++i) {
                 auto f = fs[i].get();
                 if (!f || f->size() != msgs[i].size() + 48) { ++bad; continue; }
+                if (frame_mismatch(key, msgs[i], *f)) ++mismatch;
                 frames[i] = std::move(*f);
             }
             fs.clear();
@@ -120,12 +136,12 @@ int async_mode(const std::string& policy, int T, int F) {
         });
     for (auto& x : th) x.join();
     const auto st = tx.stats(), sr = rx.stats();
-    std::printf("summary bad=%d opened=%d rejected=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu "
+    std::printf("summary bad=%d mismatch=%d opened=%d rejected=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu "
                 "rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu\n",
-                bad.load(), opened.load(), rejected.load(), (unsigned long long)st.frames,
+                bad.load(), mismatch.load(), opened.load(), rejected.load(), (unsigned long long)st.frames,
                 (unsigned long long)st.flushes, (unsigned long long)st.host_flushes, (unsigned long long)sr.frames,
                 (unsigned long long)sr.flushes, (unsigned long long)sr.host_flushes);
-    return bad ? 1 : 0;
+    return (bad || mismatch) ? 1 : 0;
 }
 
 // window <policy> <threads> <window> <frames>: every thread keeps `window` frames in flight with
@@ -137,14 +153,17 @@ int async_mode(const std::string& policy, int T, int F) {
 int window_mode(const std::string& policy, int T, int W, int F) {
     enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
                                                                                       : ENET_SCALAR_AUTO, 0);
-    FrameQueue tx;
-    FrameReceiveQueue rx;
+    // QUEUE_STRESS_MAX_FRAMES: small passes that fill (and overflow) at once
+    FrameQueueOptions opt;
+    if (const char* e = std::getenv("QUEUE_STRESS_MAX_FRAMES")) opt.max_frames = (std::size_t)std::atoll(e);
+    FrameQueue tx(opt);
+    FrameReceiveQueue rx(opt);
     std::vector<std::array<std::uint8_t, 32>> keys(T);
     for (int t = 0; t < T; ++t) {
         std::uint64_t s = 1234 + (std::uint64_t)t;
         for (auto& b : keys[t]) b = (std::uint8_t)splitmix(s);
     }
-    std::atomic<int> bad{0}, opened{0}, rejected{0};
+    std::atomic<int> bad{0}, opened{0}, rejected{0}, mismatch{0};
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t)
         th.emplace_back([&, t] {
@@ -191,6 +210,7 @@ int window_mode(const std::string& policy, int T, int W, int F) {
                 if (len != m.size() + 32 || !std::equal(m.begin(), m.end(), body.begin()) ||
                     !std::equal(mac, mac + 32, body.begin() + (std::ptrdiff_t)m.size()))
                     ++bad;
+                if (frame_mismatch(keys[t], m, *f)) ++mismatch;
                 frames[i] = std::move(*f);
             };
             for (int i = 0; i < F; ++i) {
@@ -225,19 +245,84 @@ int window_mode(const std::string& policy, int T, int W, int F) {
     const auto st = tx.stats(), sr = rx.stats();
     enet_scalar_stats ss{};
     enet_scalar_get_stats(&ss);
-    std::printf("summary bad=%d opened=%d rejected=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu "
-                "rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu evicted=%llu device_failures=%llu\n",
-                bad.load(), opened.load(), rejected.load(), (unsigned long long)st.frames,
+    std::printf("summary bad=%d mismatch=%d opened=%d rejected=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu "
+                "rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu evicted=%llu device_failures=%llu overflows=%llu\n",
+                bad.load(), mismatch.load(), opened.load(), rejected.load(), (unsigned long long)st.frames,
                 (unsigned long long)st.flushes, (unsigned long long)st.host_flushes, (unsigned long long)sr.frames,
                 (unsigned long long)sr.flushes, (unsigned long long)sr.host_flushes,
-                (unsigned long long)(st.evicted + sr.evicted), (unsigned long long)ss.device_failures);
-    return bad ? 1 : 0;
+                (unsigned long long)(st.evicted + sr.evicted), (unsigned long long)ss.device_failures,
+                (unsigned long long)(st.cas_retries + sr.cas_retries));
+    return (bad || mismatch) ? 1 : 0;
+}
+
+// split <policy> <frames> <window>: ONE reader thread submits (FrameQueue::submit) and ONE writer
+// thread collects (FrameTicket::get), the relay split of SessionManager (a socket reader hands
+// frames to a sender), at most `window` frames between them.  Every frame is checked against the
+// host engine's bytes.  AUTO must count each frame against the submitting thread only while it is
+// uncollected, wherever it is collected: a trickle stays on the host engine.
+int split_mode(const std::string& policy, int F, int W) {
+    enet_scalar_set_policy(policy == "device" ? ENET_SCALAR_DEVICE : policy == "host" ? ENET_SCALAR_HOST
+                                                                                      : ENET_SCALAR_AUTO, 0);
+    FrameQueue tx;
+    std::array<std::uint8_t, 32> key{};
+    std::uint64_t seed = 4242;
+    for (auto& b : key) b = (std::uint8_t)splitmix(seed);
+    std::vector<std::vector<std::uint8_t>> msgs(F);
+    for (auto& m : msgs) {
+        m.resize(splitmix(seed) % 1600);
+        for (auto& b : m) b = (std::uint8_t)splitmix(seed);
+    }
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<int, FrameTicket>> q;
+    int in_flight = 0;
+    std::atomic<int> bad{0}, mismatch{0};
+    std::thread reader([&] {
+        for (int i = 0; i < F; ++i) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return in_flight < W; });
+            }
+            FrameTicket t = tx.submit(key, msgs[i]);
+            std::lock_guard<std::mutex> lk(mu);
+            q.emplace_back(i, std::move(t));
+            ++in_flight;
+            cv.notify_all();
+        }
+    });
+    std::thread writer([&] {
+        for (int done = 0; done < F; ++done) {
+            std::pair<int, FrameTicket> it;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return !q.empty(); });
+                it = std::move(q.front());
+                q.pop_front();
+            }
+            auto f = it.second.get();
+            if (!f) ++bad;
+            else if (frame_mismatch(key, msgs[it.first], *f)) ++mismatch;
+            std::lock_guard<std::mutex> lk(mu);
+            --in_flight;
+            cv.notify_all();
+        }
+    });
+    reader.join();
+    writer.join();
+    const auto st = tx.stats();
+    std::printf("summary bad=%d mismatch=%d tx_frames=%llu tx_flushes=%llu tx_host_flushes=%llu\n", bad.load(),
+                mismatch.load(), (unsigned long long)st.frames, (unsigned long long)st.flushes,
+                (unsigned long long)st.host_flushes);
+    return (bad || mismatch) ? 1 : 0;
 }
 
 int main(int argc, char** argv) {
     if (argc > 1 && std::string(argv[1]) == "window")
         return window_mode(argc > 2 ? argv[2] : "device", argc > 3 ? std::atoi(argv[3]) : 16,
                            argc > 4 ? std::atoi(argv[4]) : 256, argc > 5 ? std::atoi(argv[5]) : 4000);
+    if (argc > 1 && std::string(argv[1]) == "split")
+        return split_mode(argc > 2 ? argv[2] : "auto", argc > 3 ? std::atoi(argv[3]) : 2000,
+                          argc > 4 ? std::atoi(argv[4]) : 8);
     if (argc > 1 && std::string(argv[1]) == "async")
         return async_mode(argc > 2 ? argv[2] : "device", argc > 3 ? std::atoi(argv[3]) : 8,
                           argc > 4 ? std::atoi(argv[4]) : 500);
@@ -269,7 +354,7 @@ int main(int argc, char** argv) {
     opt.max_delay = std::chrono::microseconds(200);
     FrameQueue tx(opt);
     FrameReceiveQueue rx(opt);
-    std::atomic<int> bad{0}, oversize_ok{0};
+    std::atomic<int> bad{0}, oversize_ok{0}, mismatch{0};
     {
         std::vector<std::thread> th;
         for (int t = 0; t < T; ++t)
@@ -281,6 +366,7 @@ int main(int argc, char** argv) {
                         ++bad;
                         continue;
                     }
+                    if (frame_mismatch(keys[t], msgs[t][i], *f)) ++mismatch;
                     frames[t][i] = std::move(*f);
                 }
                 // too large: refused like SessionManager::send, nothing queued
@@ -328,11 +414,11 @@ int main(int argc, char** argv) {
     const auto st = tx.stats(), sr = rx.stats();
     enet_scalar_stats ss{};
     enet_scalar_get_stats(&ss);
-    std::printf("summary bad=%d oversize_refused=%d opened=%d rejected=%d wrong=%d tx_frames=%llu tx_flushes=%llu "
+    std::printf("summary bad=%d mismatch=%d oversize_refused=%d opened=%d rejected=%d wrong=%d tx_frames=%llu tx_flushes=%llu "
                 "tx_host_flushes=%llu rx_frames=%llu rx_flushes=%llu rx_host_flushes=%llu device_failures=%llu\n",
-                bad.load(), oversize_ok.load(), opened.load(), rejected.load(), wrong.load(),
+                bad.load(), mismatch.load(), oversize_ok.load(), opened.load(), rejected.load(), wrong.load(),
                 (unsigned long long)st.frames, (unsigned long long)st.flushes, (unsigned long long)st.host_flushes,
                 (unsigned long long)sr.frames, (unsigned long long)sr.flushes, (unsigned long long)sr.host_flushes,
                 (unsigned long long)ss.device_failures);
-    return (bad || wrong || oversize_ok != T) ? 1 : 0;
+    return (bad || wrong || mismatch || oversize_ok != T) ? 1 : 0;
 }

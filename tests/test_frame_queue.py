@@ -44,7 +44,8 @@ def run(stress_bin, policy, threads=16, frames=150, seed=1):
 
 
 def check_common(rc, s, sample, threads, frames):
-    assert rc == 0 and s["bad"] == 0 and s["wrong"] == 0, s
+    # every sealed frame equals the host engine's bytes for its key, message and nonce
+    assert rc == 0 and s["bad"] == 0 and s["wrong"] == 0 and s["mismatch"] == 0, s
     assert s["oversize_refused"] == threads
     # every sealed frame reaches the send queue (the oversized ones are refused before it); every
     # opened frame reaches the receive queue except those whose length field was tampered, which
@@ -132,7 +133,7 @@ def run_async(stress_bin, policy, threads=8, frames=400):
 def check_async(rc, s, threads, frames):
     # every frame is >= 48 bytes, so byte 20 (in the body) of every 5th one is flipped
     tampered = threads * sum(1 for i in range(frames) if i % 5 == 2)
-    assert rc == 0 and s["bad"] == 0, s
+    assert rc == 0 and s["bad"] == 0 and s["mismatch"] == 0, s
     assert s["opened"] + s["rejected"] == threads * frames
     assert s["tx_frames"] == threads * frames and s["rx_frames"] == threads * frames, s
     assert s["rejected"] == tampered
@@ -170,7 +171,8 @@ def run_window(stress_bin, policy, threads=16, window=256, frames=4000):
 
 
 def check_window(rc, s, threads, frames):
-    assert rc == 0 and s["bad"] == 0, s
+    # every sealed frame equals the host engine's bytes (mismatch), and decrypts / verifies (bad)
+    assert rc == 0 and s["bad"] == 0 and s["mismatch"] == 0, s
     tampered = sum(1 for i in range(frames) if i % 9 == 4)
     foreign = sum(1 for i in range(frames) if i % 9 != 4 and i % 13 == 6) if threads > 1 else 0
     assert s["rejected"] == threads * (tampered + foreign), s
@@ -318,3 +320,67 @@ def test_queues_staged_passes_on_gpu(tmp_path):
     print(s)
     check_window(r.returncode, s, 16, 1500)
     assert s["tx_host_flushes"] == 0 and s["rx_host_flushes"] == 0 and s["device_failures"] == 0, s
+
+
+def tools_stress_bin(tmp_path):
+    from ephemeralnet_amd import build as B
+    stamp = B.read_stamp(B.LIB_TOOLS)
+    if not os.path.exists(B.LIB_TOOLS) or not stamp or stamp.get("sources_sha256") != B.source_digest(tools=True):
+        pytest.skip("tools build (ephemeralnet_amd/libenet_crypto_tools.so) missing or stale")
+    out = str(tmp_path / "queue_stress_tools")
+    subprocess.run(["g++", "-std=c++20", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"), SRC, "-o", out,
+                    "-L", os.path.dirname(B.LIB_TOOLS), "-lenet_crypto_tools",
+                    "-Wl,-rpath," + os.path.dirname(B.LIB_TOOLS)], check=True)
+    return out
+
+
+def test_stalled_overflow_submitter_on_cpu(tmp_path):
+    """a submitter whose reservation found its pass full and that is then
+    preempted must not close the pass's NEXT generation (reopened meanwhile, possibly for another
+    shard): that left the new owner's open pointer on a closed pass.  The fix ties close_full to
+    the generation read before the reservation and clears every shard that holds the pass.  This
+    run exercises that path hard on the CPU: the tools build's stand-in device runs device-style
+    passes, passes of 16 frames (QUEUE_STRESS_MAX_FRAMES=64) overflow constantly, 2 shards by
+    thread order, and ENET_QUEUE_STALL_OVERFLOW_US holds every overflowing submitter 300 us before
+    its close while passes are evicted and reopened; every frame is checked byte for byte.  (The
+    stale close did not hang here before the fix either: eviction churn soon reopens the pass for
+    some shard, which re-validates the dangling pointer -- the fix is by construction.)"""
+    out = tools_stress_bin(tmp_path)
+    env = dict(os.environ, ENET_QUEUE_FAKE_US="20", ENET_QUEUE_FAKE_COMPUTE="1", ENET_QUEUE_STALL_OVERFLOW_US="300",
+               ENET_QUEUE_SHARDS="2", ENET_QUEUE_SHARD_BY="thread", QUEUE_STRESS_MAX_FRAMES="64")
+    r = subprocess.run([out, "window", "device", "16", "128", "3000"], capture_output=True, text=True,
+                       timeout=120, env=env)
+    summ = [ln for ln in r.stdout.splitlines() if ln.startswith("summary")]
+    assert r.returncode == 0 and summ, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    s = {k: int(v) for k, v in (kv.split("=") for kv in summ[0].split()[1:])}
+    print(s)
+    check_window(r.returncode, s, 16, 3000)
+    assert s["overflows"] > 1000 and s["evicted"] > 0, s
+
+
+def test_split_submitter_collector_auto_stays_on_host_on_cpu(tmp_path):
+    """one reader thread submits, one writer thread collects, at most 8 frames
+    between them, policy auto with a (stand-in) device.  The frames are counted against the
+    submitting thread only until collected -- on the other thread -- so the trickle never reaches
+    AUTO's device threshold (320): every frame on the host engine, every byte checked."""
+    out = tools_stress_bin(tmp_path)
+    env = dict(os.environ, ENET_QUEUE_FAKE_US="60", ENET_QUEUE_FAKE_COMPUTE="1")
+    r = subprocess.run([out, "split", "auto", "3000", "8"], capture_output=True, text=True, timeout=300, env=env)
+    summ = [ln for ln in r.stdout.splitlines() if ln.startswith("summary")]
+    assert r.returncode == 0 and summ, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    s = {k: int(v) for k, v in (kv.split("=") for kv in summ[0].split()[1:])}
+    print(s)
+    assert s["bad"] == 0 and s["mismatch"] == 0
+    assert s["tx_frames"] == 3000 and s["tx_host_flushes"] == s["tx_flushes"] == 3000, s
+
+
+def test_split_submitter_collector_device_on_cpu(tmp_path):
+    """The same split under the device policy (stand-in device): the frames go through passes and
+    come back byte for byte to the collecting thread."""
+    out = tools_stress_bin(tmp_path)
+    env = dict(os.environ, ENET_QUEUE_FAKE_US="60", ENET_QUEUE_FAKE_COMPUTE="1")
+    r = subprocess.run([out, "split", "device", "2000", "64"], capture_output=True, text=True, timeout=300, env=env)
+    summ = [ln for ln in r.stdout.splitlines() if ln.startswith("summary")]
+    assert r.returncode == 0 and summ, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    s = {k: int(v) for k, v in (kv.split("=") for kv in summ[0].split()[1:])}
+    assert s["bad"] == 0 and s["mismatch"] == 0 and s["tx_frames"] == 2000 and s["tx_host_flushes"] == 0, s
