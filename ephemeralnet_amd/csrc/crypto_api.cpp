@@ -47,7 +47,17 @@
 
 // ------------------------------------------------------------------------------ scalar routing
 namespace enet::scalar {
-std::atomic<int> g_policy{ENET_SCALAR_AUTO};
+// The initial policy: ENET_SCALAR_POLICY=auto|device|host, so an unmodified binary built against
+// the reference headers (the reference's own test programs, tests/test_reference_programs.py) can
+// run on either engine; enet_scalar_set_policy changes it at run time.
+int initial_policy() {
+    const char* e = std::getenv("ENET_SCALAR_POLICY");
+    if (!e) return ENET_SCALAR_AUTO;
+    if (std::strcmp(e, "device") == 0) return ENET_SCALAR_DEVICE;
+    if (std::strcmp(e, "host") == 0) return ENET_SCALAR_HOST;
+    return ENET_SCALAR_AUTO;
+}
+std::atomic<int> g_policy{initial_policy()};
 // ChaCha20 records from this size go to the MI355X under ENET_SCALAR_AUTO.  Default: never.
 // Measured on the box: the host engine's AVX-512 keystream runs ~10 GB/s per
 // thread, i.e. as fast as the memcpy that moves a pageable caller buffer into pinned memory, so

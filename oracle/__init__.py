@@ -21,7 +21,7 @@ def build(ref: bool = False) -> None:
         subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
         # the reference's caller TUs linked against the drop-in library (needs it built first)
         if os.path.exists(os.path.join(os.path.dirname(HERE), "ephemeralnet_amd", "libenet_crypto.so")):
-            subprocess.run(["make", "-s", "-C", HERE, "dropin", "latency"], check=True)
+            subprocess.run(["make", "-s", "-C", HERE, "dropin", "latency", "reftests"], check=True)
 
 
 def lib() -> C.CDLL:
