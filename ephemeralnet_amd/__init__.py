@@ -428,8 +428,9 @@ def set_lanes_per_record(lanes: int) -> None:
 
 
 def set_staging(variant: int) -> None:
-    """Uniform-batch staging variant: 1 register prefetch (default), 3 LDS DMA / four waves per
-    SIMD, 0 per-lane path only, -1 restores the default (results are identical)."""
+    """Uniform-batch staging variant: 1 register prefetch (default), 4 without line staging,
+    5 lockstep run staging only, 0 per-lane path only, -1 restores the default (results are
+    identical)."""
     _check(lib().enet_set_staging(variant), "enet_set_staging")
 
 

@@ -17,8 +17,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libenet_crypto.so")
 OBJ = os.path.join(PKG, "build")
-# tools build: the same sources with -DENET_TOOLS_BUILD (stream-kernel probes and schedule
-# variants selectable from the environment); loaded only through ENET_LIB_PATH by tools/
+# tools build: the host TUs that read -DENET_TOOLS_BUILD (the frame queue's stand-in device and
+# stall hooks, per-phase profile, A/B knobs) recompiled with it and linked with the product's
+# kernel objects; loaded only through ENET_LIB_PATH by tools/ and the queue's stand-in-device
+# tests.  probes=True also recompiles the kernels (stream-kernel probes and schedule variants).
 LIB_TOOLS = os.path.join(PKG, "libenet_crypto_tools.so")
 OBJ_TOOLS = os.path.join(PKG, "build_tools")
 SOURCES = ["records.hip", "segments.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "duplex_split.hip",
@@ -50,6 +52,18 @@ def _headers(src: str = "") -> list[str]:
 
 def _obj(src: str, obj_dir: str = OBJ) -> str:
     return os.path.join(obj_dir, os.path.splitext(src)[0] + ".o")
+
+
+def tools_tus(probes: bool = False) -> list[str]:
+    """TUs the tools build compiles with -DENET_TOOLS_BUILD (the others are the product's)."""
+    out = []
+    for f in SOURCES:
+        if f.endswith(".hip") and not probes:
+            continue
+        with open(os.path.join(CSRC, f)) as fh:
+            if "ENET_TOOLS_BUILD" in fh.read():
+                out.append(f)
+    return out
 
 
 def source_digest(tools: bool = False) -> str:
@@ -94,18 +108,22 @@ def read_stamp(lib: str = LIB) -> dict | None:
 
 
 def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
-          tools: bool = False) -> str:
+          tools: bool = False, probes: bool = False) -> str:
     obj_dir, lib = (OBJ_TOOLS, LIB_TOOLS) if tools else (OBJ, LIB)
     cflags = CFLAGS + (["-DENET_TOOLS_BUILD"] if tools else [])
+    mine = tools_tus(probes) if tools else list(SOURCES)
+    if tools:
+        build(force=False, verbose=verbose, jobs=jobs)  # the product objects the rest links from
+    objs = {s: _obj(s, obj_dir if s in mine else OBJ) for s in SOURCES}
     os.makedirs(obj_dir, exist_ok=True)
-    digest = source_digest(tools)
+    digest = source_digest(tools) + ("+probes" if probes else "")
     stamp = read_stamp(lib) or {}
     # content, not mtimes, decides (a pushed .so beside edited sources, a checkout that reset
     # mtimes): a TU is recompiled when its own digest (flags + source + headers) differs from the
     # one the stamp recorded for the object, or the object is missing
-    tus = {s: tu_digest(s, tools) for s in SOURCES}
+    tus = {s: tu_digest(s, tools and s in mine) for s in SOURCES}
     old = stamp.get("tu_sha256", {}) if stamp.get("sources_sha256") else {}
-    todo = [s for s in SOURCES if force or old.get(s) != tus[s] or not os.path.exists(_obj(s, obj_dir))]
+    todo = [s for s in mine if force or old.get(s) != tus[s] or not os.path.exists(objs[s])]
     if not todo and os.path.exists(lib) and stamp.get("sources_sha256") == digest:
         print(f"[build] {os.path.relpath(lib, ROOT)} up to date (sources {digest[:12]}, nothing "
               "recompiled)", file=sys.stderr)
@@ -124,7 +142,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
         for f in [ex.submit(cc, s) for s in todo]:
             f.result()
     tmp = lib + ".tmp"
-    cmd = [HIPCC] + LDFLAGS + [_obj(s, obj_dir) for s in SOURCES] + ["-o", tmp]
+    cmd = [HIPCC] + LDFLAGS + [objs[s] for s in SOURCES] + ["-o", tmp]
     if verbose:
         print("[build]", " ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
@@ -142,4 +160,4 @@ def build(force: bool = False, verbose: bool = True, jobs: int | None = None,
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, tools="--tools" in sys.argv)
+    build(force="--force" in sys.argv, tools="--tools" in sys.argv, probes="--probes" in sys.argv)

@@ -83,12 +83,6 @@ enet::RecParams rec_params(const enet_records* r) {
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.lockstep = dflt ? lock : 0;
-    // ENET_LINES_LOCKSTEP=1: line staging in 512-thread lockstep workgroups (COOP 6, tuning)
-    static const int lines_lock = [] {
-        const char* e = std::getenv("ENET_LINES_LOCKSTEP");
-        return (e && e[0] == '1') ? 1 : 0;
-    }();
-    if (dflt && lines_lock) p.coop_lines = 2;
     static const int strm = [] {
         const char* e = std::getenv("ENET_STREAM");
         return (e && e[0] == '0') ? 0 : 1;
@@ -113,8 +107,6 @@ enet::RecParams rec_params(const enet_records* r) {
 #endif
 
     if (p.coop == 4) p.coop = 1;
-    // COOP 3 addresses the arena with 32-bit offsets
-    if (p.coop == 3 && p.uniform_len * (uint64_t)r->count > 0xFFFFFFFFull) p.coop = 1;
     return p;
 }
 
@@ -282,16 +274,17 @@ static std::atomic<int> g_duplex_split{-1};
 
 int duplex_split_mode() { return g_duplex_split.load(std::memory_order_relaxed); }
 
-// Uniform-batch staging: 1 = register prefetch + LDS transposition (default), 3 = LDS DMA,
-// one live keystream block, four waves per SIMD; 0 = per-lane path only.  ENET_COOP /
-// enet_set_staging override (tuning / tests).
+// Uniform-batch staging: 1 = register prefetch + LDS transposition (default: run staging in
+// lockstep 512-thread workgroups, line staging for unaligned one-lane records), 4 = plain run
+// staging, 5 = lockstep run staging; 0 = per-lane path only.  ENET_COOP / enet_set_staging
+// override (tests).  (3, the LDS-DMA four-waves-per-SIMD variant, was retired in round 6.)
 uint32_t staging_variant() {
     static const uint32_t env = [] {
         const char* s = std::getenv("ENET_COOP");
         return s ? (uint32_t)std::strtoul(s, nullptr, 10) + 1u : 0u;
     }();
     if (uint32_t f = g_staging.load(std::memory_order_relaxed)) return f - 1u;
-    if (env == 1 || env == 2 || env == 4 || env == 5 || env == 6) return env - 1u;
+    if (env == 1 || env == 2 || env == 5 || env == 6) return env - 1u;
     return 1u;
 }
 
@@ -339,8 +332,8 @@ uint32_t enet_lanes_per_record(uint32_t count, uint64_t total_bytes, uint32_t ma
 }
 
 int enet_set_staging(int variant) {
-    if (variant != -1 && variant != 0 && variant != 1 && variant != 3 && variant != 4 && variant != 5)
-        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 3, 4 or 5");
+    if (variant != -1 && variant != 0 && variant != 1 && variant != 4 && variant != 5)
+        return fail(ENET_EINVAL, "staging variant must be -1 (default), 0, 1, 4 or 5");
     enet::g_staging.store((uint32_t)(variant + 1), std::memory_order_relaxed);
     return ENET_OK;
 }

@@ -36,7 +36,7 @@ struct RecParams {
     const uint8_t* append;
     // uniform batch: every record is exactly uniform_len bytes in and out (0 = not uniform)
     uint64_t uniform_len;
-    int coop;  // uniform-batch staging variant: 0 none, 1 register prefetch, 3 LDS DMA
+    int coop;  // uniform-batch staging variant: 0 none, 1 register prefetch (default), 5 lockstep
     // COOP 1 with one lane per record and L % 128 != 0: stage whole aligned 128-byte lines
     // (COOP 4; needs 4-byte-aligned record starts and in / out starts equal mod 128)
     int coop_lines;

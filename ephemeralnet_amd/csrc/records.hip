@@ -10,17 +10,10 @@ __global__ __launch_bounds__(kWG) void records_kernel(RecParams p) {
     records_body<LOGP, MODE, FRAME, COOP>(p);
 }
 
-// 512-thread workgroups with the lockstep keystream: COOP 5 (run staging), COOP 6 (line staging)
-template <int LOGP, int MODE, int COOP>
-__global__ __launch_bounds__(512) void records_kernel_l(RecParams p) {
-    records_body<LOGP, MODE, FR_NONE, COOP>(p);
-}
-
-// COOP 3 is built to fit four waves per SIMD (<= 128 VGPRs)
+// 512-thread workgroups with the lockstep keystream (COOP 5, run staging)
 template <int LOGP, int MODE>
-__global__ __launch_bounds__(kWG) __attribute__((amdgpu_waves_per_eu(4)))
-void records_kernel_w4(RecParams p) {
-    records_body<LOGP, MODE, FR_NONE, 3>(p);
+__global__ __launch_bounds__(512) void records_kernel_l(RecParams p) {
+    records_body<LOGP, MODE, FR_NONE, 5>(p);
 }
 
 template <int LOGP, int MODE, int FRAME>
@@ -49,7 +42,7 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
     if (FRAME == FR_NONE && p.uniform_len != 0 && p.order == nullptr && p.coop >= 1) {
         // Cooperative kernels over whole workgroups of records (no dead owners, no store
         // predicates); the remaining records go through the per-lane kernel.
-        // Line staging (COOP 4/6) for one-lane records that are not 64-byte multiples: 1 M
+        // Line staging (COOP 4) for one-lane records that are not 64-byte multiples: 1 M
         // records, 1 GPU, GiB/s line vs run staging -- 1500 B 746 vs 590, 1504 B 762 vs 689,
         // 1400 B 750 vs 613; 1472 B 775 vs 789, 1536 B 835 vs 839 (tools/c3ab.sh).
         const bool lines = LOGP == 0 && p.coop == 1 && p.coop_lines && (p.uniform_len & 63u) != 0 &&
@@ -57,22 +50,18 @@ static hipError_t launch_one(const RecParams& p, hipStream_t s) {
                            p.uniform_len * (uint64_t)p.n < 0xFFFFFF00ull;
         // Lockstep keystream in 512-thread workgroups (COOP 5) unless a plain variant is asked
         // for: C2 837 -> 864, C4 868 -> 913 GiB/s; not with line staging, where it measured
-        // 765 -> 751 at C3 (COOP 6, kept for tuning) (tools/lock_ab.sh)
+        // 765 -> 751 at C3 (the line-staging lockstep variant, retired in round 6)
         const bool lock = p.coop == 5 || (p.coop == 1 && p.lockstep && !lines);
-        const uint32_t wg = (lock || (lines && p.coop_lines == 2)) ? 512u : (uint32_t)kWG;
+        const uint32_t wg = lock ? 512u : (uint32_t)kWG;
         const uint32_t per_wg = wg >> LOGP;
         const uint32_t full = p.n / per_wg;
         if (full) {
             RecParams q = p;
             q.n = full * per_wg;
-            if (lines && p.coop_lines == 2)
-                hipLaunchKernelGGL((records_kernel_l<0, MODE, 6>), dim3(full), dim3(512), 0, s, q);
-            else if (lines)
+            if (lines)
                 hipLaunchKernelGGL((records_kernel<0, MODE, FR_NONE, 4>), dim3(full), dim3(kWG), 0, s, q);
             else if (lock)
-                hipLaunchKernelGGL((records_kernel_l<LOGP, MODE, 5>), dim3(full), dim3(512), 0, s, q);
-            else if (p.coop == 3)
-                hipLaunchKernelGGL((records_kernel_w4<LOGP, MODE>), dim3(full), dim3(kWG), 0, s, q);
+                hipLaunchKernelGGL((records_kernel_l<LOGP, MODE>), dim3(full), dim3(512), 0, s, q);
             else
                 hipLaunchKernelGGL((records_kernel<LOGP, MODE, FR_NONE, 1>), dim3(full), dim3(kWG),
                                    0, s, q);

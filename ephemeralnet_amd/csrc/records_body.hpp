@@ -121,11 +121,11 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
     constexpr bool kPoly = (MODE != MODE_XOR);
     // COOP 5 = COOP 1 in 512-thread workgroups with the lockstep keystream (both waves of a SIMD
     // belong to one workgroup and meet at s_barrier every 24 ChaCha instructions)
-    // (COOP 6 = COOP 4 likewise; COOP 7 = the per-lane path of COOP 0 in 512-thread workgroups,
-    // the streaming kernel's fallback)
-    constexpr uint32_t WGS = (COOP == 5 || COOP == 6 || COOP == 7) ? 512u : (uint32_t)kWG;
+    // (COOP 7 = the per-lane path of COOP 0 in 512-thread workgroups, the streaming kernel's
+    // fallback)
+    constexpr uint32_t WGS = (COOP == 5 || COOP == 7) ? 512u : (uint32_t)kWG;
     __shared__ __attribute__((aligned(16))) uint8_t
-        slab[(COOP == 4 || COOP == 6) ? WGS * kRing : (COOP && COOP != 7) ? WGS * kRun : 16];
+        slab[COOP == 4 ? WGS * kRing : (COOP && COOP != 7) ? WGS * kRun : 16];
 
     const uint32_t gid = blockIdx.x * WGS + threadIdx.x;
     const uint32_t group = gid >> LOGP;
@@ -479,7 +479,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             ctail = cend;
         }
     }
-    if (COOP == 4 || COOP == 6) {
+    if (COOP == 4) {
         // Line-aligned staging for uniform batches whose records are not 128-byte aligned
         // (C3: 1 500-byte records), one lane per record.  Run s of a record = record bytes
         // [128s, 128s+128) straddles two arena lines (offset d = record start mod 128), so
@@ -632,8 +632,7 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             if (rl == kRun) {
                 if (MODE == MODE_OPEN) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
                 uint32_t ka[16], kb[16];
-                if (COOP == 6) chacha_block2_lockstep(R, c0, c0 + 1, ka, kb);
-                else chacha_block2(R, c0, c0 + 1, ka, kb);
+                chacha_block2(R, c0, c0 + 1, ka, kb);
 #pragma unroll
                 for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
                 if (MODE == MODE_SEAL) { poly_block64(h, PR, x); poly_block64(h, PR, x + 16); }
@@ -695,104 +694,6 @@ __device__ __forceinline__ void records_body(const RecParams& p) {
             poly_setup();
         }
     }
-    if (COOP == 3) {
-        // Same whole-line stages and wave-private slab as COOP 1, but the loads go straight to
-        // LDS (global_load_lds_dwordx4: lane-linear destination, the chunk swizzle rides on the
-        // source address), nothing is prefetched into registers and only ONE keystream block
-        // is live at a time: the kernel fits in <= 128 VGPRs (four waves per SIMD).  The
-        // keystream does not depend on the data, so each stage's DMA flies under the rounds of
-        // its first block; block 1's own-run reads are issued before its keystream is computed.
-        // 32-bit offsets from the arena bases (the host launches it only for batches < 4 GiB),
-        // so loads and stores take the SGPR-base + VGPR-offset form.
-        const uint32_t lane = threadIdx.x & 63u;
-        const uint32_t wbase = threadIdx.x & ~63u;
-        const uint64_t Lu = p.uniform_len;
-        const uint32_t nfull = (uint32_t)(Lu >> 6);
-        const uint32_t jl = P - 1;
-        const uint32_t fmin = (nfull > jl * B) ? min(B, nfull - jl * B) : 0u;
-        const uint32_t Ts = lay_ok ? fmin / kStage : 0u;
-        const uint32_t kk = lane & 7u;
-        const uint32_t wgid0 = blockIdx.x * kWG + wbase;
-        uint32_t off[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const uint32_t o = 8u * i + (lane >> 3);
-            const uint32_t og = (wgid0 + o) >> LOGP;
-            const uint32_t oj = (wgid0 + o) & (P - 1);
-            const uint32_t sw = slab_sw(o);
-            off[i] = (uint32_t)((uint64_t)og * Lu + 64ull * oj * B + 16u * (kk ^ sw));
-        }
-        const uint8_t* ibase = p.in + (p.n ? p.in_off[0] : 0);
-        uint8_t* obase = p.out + (p.n ? p.out_off[0] : 0);
-        uint8_t* wslab = slab + wbase * kRun;
-        uint8_t* myrun = slab + threadIdx.x * kRun;
-        const uint32_t msw = slab_sw(lane);
-        auto dma = [&](uint32_t stage) {
-            const uint32_t adv = kRun * stage;
-#pragma unroll
-            for (int i = 0; i < 8; ++i)
-                __builtin_amdgcn_global_load_lds(
-                    (__attribute__((address_space(1))) const void*)(ibase + (off[i] + adv)),
-                    (__attribute__((address_space(3))) void*)(wslab + 1024u * i), 16, 0, 0);
-        };
-        auto read_own = [&](int b, uint32_t d[16]) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * ((4u * b + k) ^ msw));
-                d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
-            }
-        };
-        auto finish_block = [&](int b, uint32_t d[16], const uint32_t ks[16]) {
-            if (MODE == MODE_OPEN) poly_block64(h, PR, d);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) d[i] ^= ks[i];
-            if (MODE == MODE_SEAL) poly_block64(h, PR, d);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                *reinterpret_cast<uint4*>(myrun + 16u * ((4u * b + k) ^ msw)) =
-                    make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
-        };
-        if (Ts > 0) dma(0);
-        poly_setup();
-        for (uint32_t st = 0; st < Ts; ++st) {
-            const uint32_t c0 = ctr0 + cbeg + kStage * st;
-            uint32_t d[16], ks[16];
-            chacha_block(R, c0, ks);
-            ENET_PIN16(ks);
-            // the stage has landed (this also retires the previous stage's stores)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            ENET_WAVE_LDS_SYNC();
-            read_own(0, d);
-            finish_block(0, d, ks);
-            read_own(1, d);
-            ENET_WAVE_LDS_SYNC();
-            chacha_block(R, c0 + 1, ks);
-            ENET_PIN16(ks);
-            finish_block(1, d, ks);
-            ENET_WAVE_LDS_SYNC();
-            const uint32_t adv = kRun * st;
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                uint32_t v[16];  // plain words: a uint4 array would be kept in scratch
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 t =
-                        *reinterpret_cast<const uint4*>(wslab + 1024u * (4 * hh + i) + 16u * lane);
-                    v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    *reinterpret_cast<uint4*>(obase + (off[4 * hh + i] + adv)) =
-                        make_uint4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-            }
-            // the stores above consumed every lane-linear read: the slab is free for the next
-            // stage's DMA
-            ENET_WAVE_LDS_SYNC();
-            if (st + 1 < Ts) dma(st + 1);
-        }
-        cco = min(cfast, cbeg + kStage * Ts);
-    }
-
     // ---- fast path: whole blocks, next block prefetched while this one is computed
     uint32_t w[16];
     if (cco < cfast) load_full(src + 64ull * cco, w);

@@ -377,8 +377,9 @@ ENET_API int enet_set_seg_min(int64_t bytes);
 ENET_API uint64_t enet_seg_batches(void);
 /* Staging of uniform-length batches (all records the same length): 1 = register prefetch + LDS
  * transposition (default; records that are not 128-byte aligned and get one lane each are staged
- * as whole aligned 128-byte lines), 4 = 1 without the line staging, 3 = LDS DMA with one live
- * keystream block (four waves per SIMD), 0 = per-lane path only, -1 restores the default.
+ * as whole aligned 128-byte lines; the rest in lockstep 512-thread workgroups), 4 = 1 without the
+ * line staging, 5 = lockstep run staging only, 0 = per-lane path only, -1 restores the default.
+ * (3, the LDS-DMA variant, was retired: it is refused.)
  * Results are identical; tuning / test knob. */
 ENET_API int enet_set_staging(int variant);
 /* ---- scalar C++ drop-in routing (include/ephemeralnet/crypto/{ChaCha20,Sha256,HmacSha256,

@@ -94,8 +94,10 @@ def test_library_loads_and_host_helpers(built):
     E.set_lanes_per_record(0)
     with pytest.raises(E.EnetError):
         E.set_staging(2)
-    E.set_staging(3)
+    with pytest.raises(E.EnetError):
+        E.set_staging(3)  # the LDS-DMA variant, retired in round 6
     E.set_staging(4)
+    E.set_staging(5)
     E.set_staging(-1)
     # host-memory runtime modes 0, 3, 4 and -1 = auto (enet_host_set_mode); the retired 1 / 2
     # and anything else are refused with the mode kept

@@ -20,6 +20,8 @@
 #   sessions   the reference's thread-per-session load (SessionManager.cpp:331-332, 337-388, 822):
 #              T session threads, each with ONE blocking frame in flight (queue_bench sync), device
 #              queue vs host engine vs auto, T = ${THREADS:-64 256 768}, two rounds
+#   long-prof  the long-record side leg (1 x 32 MiB, 8 x 1 MiB; bench.py --long-only) plain and
+#              under a rocprofv3 kernel trace (per-kernel durations, launch gaps)
 # Round-wide evidence (kernel stats, PMC, side configs): tools/gpu_round.sh.
 set -euo pipefail
 R=${1:?recipe}
@@ -150,6 +152,11 @@ sessions)
     QUEUE_BENCH_WARMUP=${WARMUP:-0.3} timeout -k 10 90 taskset -c $CPUS tools/queue_bench $pol sync $t 1 1.0 >> $O/sessions.jsonl 2>> $O/sessions.err
   done; done; done
   qsummary $O/sessions.jsonl ;;
+long-prof)
+  timeout -k 10 180 python bench.py --long-only > $O/long.json 2> $O/long.err
+  cut -c1-600 $O/long.json
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_long -o long -- python bench.py --long-only > $O/long_prof.json 2> $O/long_prof.err
+  find $O/prof_long -name "*kernel_stats.csv" -exec cat {} \; ;;
 *)
   echo "unknown recipe $R" >&2; exit 2 ;;
 esac
