@@ -1001,6 +1001,63 @@ def pow_bench(args) -> dict:
     return out
 
 
+def chunk_leg(E, dev, stream, pt, offs, keys, nonces, lens, reps: int = 3) -> dict:
+    """Chunk store + fetch (caller-given ids) of the long records through the C ABI, device-resident
+    -- the hash chains on host threads, the cipher on the tiles (capi.cpp chunk_*_host_hash) --
+    against the host engine doing the same on the calling thread's core (enet_host_sha256 +
+    enet_host_chacha20_xor per chunk, store then fetch: Node.cpp:1414-1417, 1644-1655).  ms per
+    store+fetch pair, best of `reps`."""
+    import ctypes as C
+    import time
+    import numpy as np
+    import torch
+    n, tot = len(lens), sum(lens)
+    g = torch.Generator(device=dev).manual_seed(91)
+    ids = torch.randint(0, 256, (32 * n,), dtype=torch.uint8, device=dev, generator=g)
+    ct, back = torch.empty_like(pt), torch.empty_like(pt)
+    hashes = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    sb = E.Batch(pt, offs, keys, nonces, total_bytes_hint=tot, max_len_hint=max(lens))
+    ob = E.Batch(ct, offs, keys, nonces, total_bytes_hint=tot, max_len_hint=max(lens))
+    best = None
+    good = True
+    for _ in range(reps + 1):  # the first pair warms the pinned buffers and worker streams
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        E.chunk_store(sb, ct, hashes, chunk_ids=ids, stream=stream)
+        E.chunk_fetch(ob, back, ids, hashes, ok, stream=stream)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) * 1e3
+        best = ms if best is None or ms < best else best
+        good = good and int(ok.sum()) == n and torch.equal(back, pt)
+    L = E.lib()
+    L.enet_host_sha256.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
+    L.enet_host_chacha20_xor.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64]
+    hp = pt.cpu().numpy()
+    hk, hn, hid = keys.cpu().numpy(), nonces.cpu().numpy(), ids.cpu().numpy()
+    ho = np.empty_like(hp)
+    hb = np.empty_like(hp)
+    dg = np.empty(32, np.uint8)
+    o = offs.cpu().tolist()
+    host_best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for i in range(n):
+            a, L_ = o[i], o[i + 1] - o[i]
+            ctr = int.from_bytes(hid[32 * i:32 * i + 4].tobytes(), "little")
+            L.enet_host_sha256(hp[a:].ctypes.data, L_, dg.ctypes.data)
+            L.enet_host_chacha20_xor(hk[32 * i:].ctypes.data, hn[12 * i:].ctypes.data, ctr, hp[a:].ctypes.data,
+                                     ho[a:].ctypes.data, L_)
+            L.enet_host_chacha20_xor(hk[32 * i:].ctypes.data, hn[12 * i:].ctypes.data, ctr, ho[a:].ctypes.data,
+                                     hb[a:].ctypes.data, L_)
+            L.enet_host_sha256(hb[a:].ctypes.data, L_, dg.ctypes.data)
+        ms = (time.perf_counter() - t0) * 1e3
+        host_best = ms if host_best is None or ms < host_best else host_best
+    return {"chunk_store_fetch_ms": round(best, 3), "chunk_store_fetch_ok": bool(good),
+            "chunk_host_engine_ms": round(host_best, 3), "chunk_host_threads": E.host_cpu_budget(),
+            "chunk_vs_host_engine": round(host_best / best, 2)}
+
+
 def long_records_leg(dev, reps: int = 20) -> dict:
     """Side leg (never `value`): the reference's real chunk sizes, device-resident -- a stored file
     is ONE chunk of up to 32 MiB (Config.hpp:62, Node.cpp:1414-1417) and session payloads go up
@@ -1052,10 +1109,13 @@ def long_records_leg(dev, reps: int = 20) -> dict:
                 row[f"{mode}_{path}_ms"] = round(ms, 4)
                 row[f"{mode}_{path}_ok"] = bool(good)
         E.set_seg_min(-1)
+        row.update(chunk_leg(E, dev, stream, pt, offs, keys, nonces, lens))
         res[name] = row
     res["is"] = ("device-resident, per-record (key, nonce); GiB/s = plaintext bytes / (seal + open) "
                  "time; tiles = 64 KiB tiles over every CU (default), record_engine = at most 16 lanes "
-                 "per record (enet_set_seg_min(INT64_MAX))")
+                 "per record (enet_set_seg_min(INT64_MAX)); chunk_store_fetch_ms = one chunk store + fetch pair "
+                 "through the C ABI (hash chains on host threads, cipher on the tiles, wall clock), "
+                 "chunk_host_engine_ms = the host engine doing both on one core")
     return res
 
 

@@ -58,7 +58,7 @@ EXPORTS = [
     "enet_aead_hmac_seal_batch",
     "enet_aead_hmac_open_batch", "enet_chunk_counter",
     "enet_lanes_per_record", "enet_set_lanes_per_record", "enet_set_staging", "enet_set_duplex_split",
-    "enet_set_seg_min", "enet_seg_batches", "enet_last_error",
+    "enet_set_seg_min", "enet_seg_batches", "enet_set_host_hash_min", "enet_host_hash_batches", "enet_last_error",
     "enet_abi_version", "enet_pipeline_create", "enet_pipeline_destroy",
     "enet_pipeline_chacha20_xor", "enet_pipeline_aead_seal", "enet_pipeline_aead_open",
     "enet_pipeline_aead_hmac_seal", "enet_pipeline_aead_hmac_open", "enet_pipeline_wire_seal",
@@ -159,6 +159,8 @@ def lib() -> C.CDLL:
         L.enet_set_duplex_split.argtypes = [C.c_int]
         L.enet_set_seg_min.argtypes = [C.c_int64]
         L.enet_seg_batches.restype = C.c_uint64
+        L.enet_set_host_hash_min.argtypes = [C.c_int64]
+        L.enet_host_hash_batches.restype = C.c_uint64
         L.enet_last_error.restype = C.c_char_p
         L.enet_pipeline_create.argtypes = [C.c_int, u64, u32]
         L.enet_pipeline_create.restype = vp
@@ -273,6 +275,19 @@ def seg_batches() -> int:
 
 SEG_MIN = 256 << 10
 SEG_NEVER = (1 << 63) - 1
+
+
+def set_host_hash_min(nbytes: int) -> None:
+    """enet_set_host_hash_min: chunk store / fetch records of at least nbytes hash on host
+    threads while the device ciphers them (-1 automatic; 2**63-1 never: every chain on the GPU)."""
+    _check(lib().enet_set_host_hash_min(int(nbytes)), "enet_set_host_hash_min")
+
+
+def host_hash_batches() -> int:
+    return int(lib().enet_host_hash_batches())
+
+
+HOST_HASH_MIN = 256 << 10
 
 
 def chacha20_xor(b: Batch, out, counters=None, out_offsets=None, stream=None) -> None:

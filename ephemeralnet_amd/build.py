@@ -24,7 +24,7 @@ OBJ = os.path.join(PKG, "build")
 LIB_TOOLS = os.path.join(PKG, "libenet_crypto_tools.so")
 OBJ_TOOLS = os.path.join(PKG, "build_tools")
 SOURCES = ["records.hip", "segments.hip", "stream.hip", "sha.hip", "pow.hip", "duplex.hip", "duplex_split.hip",
-           "capi.cpp", "crypto_api.cpp", "pipeline.cpp", "host_engine.cpp", "frame_queue.cpp", "host_batch.cpp",
+           "capi.cpp", "chunk_hybrid.cpp", "crypto_api.cpp", "pipeline.cpp", "host_engine.cpp", "frame_queue.cpp", "host_batch.cpp",
            "host_topo.cpp"]
 HEADERS = ["enet_device.hpp", "enet_internal.hpp", "records_body.hpp", "stream_common.hpp", "host_engine.hpp",
            "scalar.hpp", "host_batch.hpp", "host_topo.hpp"]

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "enet_internal.hpp"
 
@@ -191,9 +192,10 @@ struct SegRun {
     const uint8_t* claimed = nullptr;
 };
 
-// Plan + tile kernels for the batch's long records; sr.claimed marks them for the record engine
+// Plan + tile kernels for the batch's long records; sr.claimed marks them for the record engine.
+// index_n: one past the largest record index (r->count unless r->order names a subset).
 int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long_min, hipStream_t st,
-              SegRun& sr) {
+              SegRun& sr, uint32_t index_n) {
     const uint32_t n = r->count;
     const uint64_t total = r->total_bytes_hint ? r->total_bytes_hint
                                                : (uint64_t)std::min<uint32_t>(n, 1024u) * r->max_len_hint;
@@ -201,7 +203,7 @@ int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long
     const uint64_t ecap = std::min<uint64_t>(n, long_min ? total / long_min + 1 : n);
     const uint64_t tcap = std::min<uint64_t>(total / enet::kSegTileBytes + ecap + 1, 0xFFFFFFFFull);
     const size_t o_ent = 256, o_cl = o_ent + (size_t)ecap * sizeof(enet::SegEntry),
-                 o_part = (o_cl + n + 255) & ~size_t(255), bytes = o_part + (size_t)tcap * 32;
+                 o_part = (o_cl + index_n + 255) & ~size_t(255), bytes = o_part + (size_t)tcap * 32;
     hipMemPool_t pool = seg_pool();
     if (!pool) return fail(ENET_EHIP, "sequence-parallel scratch: no memory pool for the current device");
     if (hipError_t e = hipMallocFromPoolAsync(&sr.mem, bytes, pool, st)) {
@@ -226,6 +228,7 @@ int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long
     q.tag_in = p.tag_in;
     q.tag_out = p.tag_out;
     q.ok = p.ok;
+    q.order = p.order;
     q.hdr = reinterpret_cast<unsigned long long*>(base);
     q.entries = reinterpret_cast<enet::SegEntry*>(base + o_ent);
     q.claimed = base + o_cl;
@@ -246,11 +249,12 @@ void seg_end(SegRun& sr, hipStream_t st) {
 }
 
 // The record engine over the batch, with the long records on the tiles first when seg_wanted
-int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t st, const char* what) {
+int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t st, const char* what,
+                uint32_t index_n = 0) {
     uint64_t long_min = 0;
     SegRun sr;
     if (mode <= enet::MODE_OPEN && seg_wanted(r, long_min)) {
-        if (int e = seg_begin(mode, r, p, long_min, st, sr)) {
+        if (int e = seg_begin(mode, r, p, long_min, st, sr, index_n ? index_n : r->count)) {
             seg_end(sr, st);
             return e;
         }
@@ -260,6 +264,263 @@ int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t
     const int rc = hip_status(enet::launch_records(mode, p, lanes_for(r), st), what);
     seg_end(sr, st);
     return rc;
+}
+
+// ---- chunk store / fetch on the device (every record on the GPU)
+int chunk_store_device(const enet_records* r, const uint8_t* chunk_ids, uint8_t* chunk_hashes,
+                              hipStream_t st) {
+    if (chunk_ids && duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.chunk_ids = chunk_ids;
+        d.digests = chunk_hashes;
+        return hip_status(enet::launch_duplex(enet::DK_CHUNK, false, d, st), "chunk_store duplex");
+    }
+    // 1) chunk_hash = SHA-256(pt) (Node.cpp:1414; = derive_chunk_id, StoreProof.cpp:75-78)
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->in;
+    s.off = r->in_offsets;
+    s.digest = chunk_hashes;
+    s.order = r->order;
+    if (int e = hip_status(enet::launch_sha(s, st), "chunk_store sha")) return e;
+    // 2) ChaCha20 from counter LE32(chunk_id[0..3]) (CryptoManager.cpp:8-13,38-46), the id read
+    //    on the device (the fresh digests when the caller derives ids from content)
+    enet::RecParams p = rec_params(r);
+    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids ? chunk_ids : chunk_hashes);
+    p.counter_stride = 8;
+    return hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
+                      "chunk_store chacha");
+}
+
+int chunk_fetch_device(const enet_records* r, const uint8_t* chunk_ids, const uint8_t* chunk_hashes,
+                              uint8_t* ok, hipStream_t st) {
+    if (duplex_on()) {
+        enet::DuplexParams d = duplex_params(r);
+        d.chunk_ids = chunk_ids;
+        d.expect = chunk_hashes;
+        d.ok = ok;
+        return hip_status(enet::launch_duplex(enet::DK_CHUNK, true, d, st), "chunk_fetch duplex");
+    }
+    // 1) decrypt_with_key (CryptoManager.cpp:49-58)
+    enet::RecParams p = rec_params(r);
+    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids);
+    p.counter_stride = 8;
+    if (int e = hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
+                           "chunk_fetch chacha"))
+        return e;
+    // 2) SHA-256(pt) == manifest.chunk_hash, else no plaintext (Node.cpp:1644-1655)
+    enet::ShaParams s{};
+    s.n = r->count;
+    s.in = r->out;
+    s.off = r->out_offsets;
+    s.expect = chunk_hashes;
+    s.ok = ok;
+    s.zero_on_fail = r->out;
+    s.order = r->order;
+    return hip_status(enet::launch_sha(s, st), "chunk_fetch sha verify");
+}
+
+
+// ---- long chunks: the cipher on the device, the hash chain on host threads (chunk_hybrid.cpp)
+// A record of >= kHostHashMin bytes is one serial SHA-256 chain: ~34 MB/s on a GPU lane (the 64 KiB
+// duplex chain takes 1.90 ms) against ~2.1 GB/s on a SHA-NI core (490 us per MiB).
+// The host route pays while the host's chains (sum over T threads) finish before the GPU's
+// longest lane would: sum(long) / (T * 2.1 GB/s) < Lmax / 34 MB/s, i.e. sum(long) < ~60 T Lmax.
+// Everything shorter stays on the one-pass duplex kernel.
+constexpr uint64_t kHostHashMin = 256u << 10;
+constexpr uint64_t kHostHashRatio = 60;
+std::atomic<int64_t> g_hh_min{-1};  // enet_set_host_hash_min: -1 auto, else forced (INT64_MAX never)
+std::atomic<uint64_t> g_hh_batches{0};
+
+uint32_t host_hash_threads() {
+    static const uint32_t t = [] {
+        const uint32_t b = enet_host_cpu_budget();
+        return b ? b : 1u;
+    }();
+    return t;
+}
+
+struct HostPinned {  // thread-local pinned scratch, grow-only
+    void* p = nullptr;
+    size_t cap = 0;
+    ~HostPinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    uint8_t* get(size_t n) {
+        if (n > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+            cap = n;
+        }
+        return static_cast<uint8_t*>(p);
+    }
+};
+thread_local HostPinned t_pinned;
+
+struct LongSplit {
+    std::vector<uint64_t> in_off, out_off;
+    std::vector<uint32_t> shorts, longs;
+    uint64_t short_max = 0, short_sum = 0, long_max = 0, long_sum = 0;
+};
+
+// 1: the batch has long chunks for the host route (ls filled), 0: not, < 0: error
+int long_split(const enet_records* r, hipStream_t st, LongSplit& ls) {
+    const int64_t f = g_hh_min.load(std::memory_order_relaxed);
+    if (f == INT64_MAX || r->order) return 0;  // a caller-ordered subset keeps its own schedule
+    const uint64_t lmin = f >= 0 ? (uint64_t)f : kHostHashMin;
+    if (f < 0 && r->max_len_hint && r->max_len_hint < lmin) return 0;  // hint: nothing that long
+    const uint32_t n = r->count;
+    ls.in_off.resize(n + 1);
+    ls.out_off.resize(n + 1);
+    if (hipError_t e = hipMemcpyAsync(ls.in_off.data(), r->in_offsets, 8ull * (n + 1), hipMemcpyDeviceToHost, st))
+        return hip_status(e, "chunk: offsets to host");
+    if (hipError_t e = hipMemcpyAsync(ls.out_off.data(), r->out_offsets, 8ull * (n + 1), hipMemcpyDeviceToHost, st))
+        return hip_status(e, "chunk: offsets to host");
+    if (hipError_t e = hipStreamSynchronize(st)) return hip_status(e, "chunk: offsets to host");
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t a = ls.in_off[i], b = ls.in_off[i + 1];
+        const uint64_t L = b >= a ? b - a : 0;
+        if (b >= a && L >= lmin && ls.out_off[i + 1] >= ls.out_off[i]) {
+            ls.longs.push_back(i);
+            ls.long_max = std::max(ls.long_max, L);
+            ls.long_sum += L;
+        } else {
+            ls.shorts.push_back(i);
+            ls.short_max = std::max(ls.short_max, L);
+            ls.short_sum += L;
+        }
+    }
+    if (ls.longs.empty()) return 0;
+    if (f < 0 && ls.long_sum > kHostHashRatio * host_hash_threads() * ls.long_max) return 0;  // GPU lanes win
+    return 1;
+}
+
+// device scratch: the two index lists (and room for host results), stream-ordered from the pool
+struct ChunkScratch {
+    uint8_t* dev = nullptr;
+    uint8_t* host = nullptr;
+    uint32_t* d_shorts = nullptr;
+    uint32_t* d_longs = nullptr;
+    uint8_t* d_res = nullptr;  // [m][32] digests / [m] verdicts from the host
+    uint8_t* h_res = nullptr;
+};
+
+int chunk_scratch(const LongSplit& ls, hipStream_t st, ChunkScratch& cs) {
+    const size_t ns = ls.shorts.size(), m = ls.longs.size();
+    const size_t o_l = (4 * ns + 255) & ~size_t(255), o_r = (o_l + 4 * m + 255) & ~size_t(255),
+                 bytes = o_r + 32 * m;
+    hipMemPool_t pool = seg_pool();
+    if (!pool) return fail(ENET_EHIP, "chunk: no memory pool for the current device");
+    void* d = nullptr;
+    if (hipError_t e = hipMallocFromPoolAsync(&d, bytes, pool, st)) return hip_status(e, "chunk scratch");
+    cs.dev = static_cast<uint8_t*>(d);
+    cs.host = t_pinned.get(bytes);
+    if (!cs.host) return fail(ENET_EHIP, "chunk: pinned host scratch");
+    std::memcpy(cs.host, ls.shorts.data(), 4 * ns);
+    std::memcpy(cs.host + o_l, ls.longs.data(), 4 * m);
+    cs.d_shorts = reinterpret_cast<uint32_t*>(cs.dev);
+    cs.d_longs = reinterpret_cast<uint32_t*>(cs.dev + o_l);
+    cs.d_res = cs.dev + o_r;
+    cs.h_res = cs.host + o_r;
+    return hip_status(hipMemcpyAsync(cs.dev, cs.host, o_r, hipMemcpyHostToDevice, st), "chunk: index lists");
+}
+
+// the end of a host-route call: scratch back to the pool, and the stream drained (the pinned
+// scratch is this thread's and is reused by its next call)
+int chunk_finish(ChunkScratch& cs, hipStream_t st, int rc) {
+    if (cs.dev) (void)hipFreeAsync(cs.dev, st);
+    const hipError_t e = hipStreamSynchronize(st);
+    return rc ? rc : hip_status(e, "chunk: drain");
+}
+
+enet_records subset(const enet_records* r, const uint32_t* order, uint32_t count, uint64_t max_len, uint64_t sum) {
+    enet_records q = *r;
+    q.count = count;
+    q.order = order;
+    q.max_len_hint = (uint32_t)std::min<uint64_t>(max_len, 0xFFFFFFFFu);
+    q.total_bytes_hint = sum;
+    return q;
+}
+
+int chunk_store_host_hash(const enet_records* r, const uint8_t* ids, uint8_t* hashes, hipStream_t st,
+                          const LongSplit& ls) {
+    ChunkScratch cs;
+    int rc = chunk_scratch(ls, st, cs);
+    const uint32_t m = (uint32_t)ls.longs.size();
+    // the short chunks' one-pass kernel runs while the host hashes the long ones
+    if (!rc && !ls.shorts.empty()) {
+        enet_records q = subset(r, cs.d_shorts, (uint32_t)ls.shorts.size(), ls.short_max, ls.short_sum);
+        rc = chunk_store_device(&q, ids, hashes, st);
+    }
+    std::string err;
+    if (!rc && enet::host_hash_records(r->in, ls.in_off.data(), ls.longs.data(), m, nullptr, host_hash_threads(),
+                                       cs.h_res, err))
+        rc = fail(ENET_EHIP, ("chunk_store: " + err).c_str());
+    if (!rc) rc = hip_status(hipMemcpyAsync(cs.d_res, cs.h_res, 32ull * m, hipMemcpyHostToDevice, st), "chunk_store: digests");
+    if (!rc) rc = hip_status(enet::launch_scatter(cs.d_res, cs.d_longs, m, hashes, 32, st), "chunk_store: digests");
+    if (!rc) {
+        // ChaCha20 from LE32(id) -- the fresh digest when the id is derived from content
+        // (CryptoManager.cpp:8-13, Node.cpp:1414-1417) -- over the long chunks, on the tiles
+        enet_records q = subset(r, cs.d_longs, m, ls.long_max, ls.long_sum);
+        enet::RecParams p = rec_params(&q);
+        p.counters = reinterpret_cast<const uint32_t*>(ids ? ids : hashes);
+        p.counter_stride = 8;
+        rc = run_records(enet::MODE_XOR, &q, p, st, "chunk_store long chacha", r->count);
+    }
+    g_hh_batches.fetch_add(1, std::memory_order_relaxed);
+    return chunk_finish(cs, st, rc);
+}
+
+int chunk_fetch_host_hash(const enet_records* r, const uint8_t* ids, const uint8_t* expect, uint8_t* ok,
+                          hipStream_t st, const LongSplit& ls) {
+    ChunkScratch cs;
+    int rc = chunk_scratch(ls, st, cs);
+    const uint32_t m = (uint32_t)ls.longs.size(), n = r->count;
+    if (!rc && !ls.shorts.empty()) {
+        enet_records q = subset(r, cs.d_shorts, (uint32_t)ls.shorts.size(), ls.short_max, ls.short_sum);
+        rc = chunk_fetch_device(&q, ids, expect, ok, st);
+    }
+    if (!rc) {  // decrypt_with_key (CryptoManager.cpp:49-58) over the long chunks, on the tiles
+        enet_records q = subset(r, cs.d_longs, m, ls.long_max, ls.long_sum);
+        enet::RecParams p = rec_params(&q);
+        p.counters = reinterpret_cast<const uint32_t*>(ids);
+        p.counter_stride = 8;
+        rc = run_records(enet::MODE_XOR, &q, p, st, "chunk_fetch long chacha", n);
+    }
+    // the expected hashes to the host, then the plaintext in pieces as the host hashes it
+    std::vector<uint8_t> want(32ull * n);
+    hipEvent_t ready = nullptr;
+    if (!rc) rc = hip_status(hipMemcpyAsync(want.data(), expect, 32ull * n, hipMemcpyDeviceToHost, st), "chunk_fetch: hashes");
+    if (!rc) rc = hip_status(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "chunk_fetch: event");
+    if (!rc) rc = hip_status(hipEventRecord(ready, st), "chunk_fetch: event");
+    std::string err;
+    if (!rc && enet::host_hash_records(r->out, ls.out_off.data(), ls.longs.data(), m, ready, host_hash_threads(),
+                                       cs.h_res, err))
+        rc = fail(ENET_EHIP, ("chunk_fetch: " + err).c_str());
+    if (!rc) rc = hip_status(hipEventSynchronize(ready), "chunk_fetch: hashes");
+    if (ready) (void)hipEventDestroy(ready);
+    if (!rc) {
+        // SHA-256(pt) == manifest.chunk_hash, else no plaintext (Node.cpp:1644-1655); a chunk
+        // whose output length differs from its input fails too
+        std::vector<uint8_t> okl(m);
+        for (uint32_t k = 0; k < m && !rc; ++k) {
+            const uint32_t i = ls.longs[k];
+            const bool same_len = ls.out_off[i + 1] - ls.out_off[i] == ls.in_off[i + 1] - ls.in_off[i];
+            okl[k] = same_len && std::memcmp(cs.h_res + 32ull * k, want.data() + 32ull * i, 32) == 0;
+            if (!okl[k])
+                rc = hip_status(hipMemsetAsync(r->out + ls.out_off[i], 0, ls.out_off[i + 1] - ls.out_off[i], st),
+                                "chunk_fetch: zero failed chunk");
+        }
+        if (!rc) {
+            std::memcpy(cs.h_res, okl.data(), m);  // digests consumed: the verdicts go up from here
+            rc = hip_status(hipMemcpyAsync(cs.d_res, cs.h_res, m, hipMemcpyHostToDevice, st), "chunk_fetch: verdicts");
+        }
+        if (!rc) rc = hip_status(enet::launch_scatter(cs.d_res, cs.d_longs, m, ok, 1, st), "chunk_fetch: verdicts");
+    }
+    g_hh_batches.fetch_add(1, std::memory_order_relaxed);
+    return chunk_finish(cs, st, rc);
 }
 
 }  // namespace
@@ -574,27 +835,11 @@ int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids, uint
         return fail(ENET_EINVAL, "chunk_store: chunk_hashes NULL or misaligned");
     if (chunk_ids && !aligned4(chunk_ids)) return fail(ENET_EINVAL, "chunk_store: chunk_ids misaligned");
     hipStream_t st = (hipStream_t)stream;
-    if (chunk_ids && duplex_on()) {
-        enet::DuplexParams d = duplex_params(r);
-        d.chunk_ids = chunk_ids;
-        d.digests = chunk_hashes;
-        return hip_status(enet::launch_duplex(enet::DK_CHUNK, false, d, st), "chunk_store duplex");
-    }
-    // 1) chunk_hash = SHA-256(pt) (Node.cpp:1414; = derive_chunk_id, StoreProof.cpp:75-78)
-    enet::ShaParams s{};
-    s.n = r->count;
-    s.in = r->in;
-    s.off = r->in_offsets;
-    s.digest = chunk_hashes;
-    s.order = r->order;
-    if (int e = hip_status(enet::launch_sha(s, st), "chunk_store sha")) return e;
-    // 2) ChaCha20 from counter LE32(chunk_id[0..3]) (CryptoManager.cpp:8-13,38-46), the id read
-    //    on the device (the fresh digests when the caller derives ids from content)
-    enet::RecParams p = rec_params(r);
-    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids ? chunk_ids : chunk_hashes);
-    p.counter_stride = 8;
-    return hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
-                      "chunk_store chacha");
+    LongSplit ls;
+    const int route = long_split(r, st, ls);
+    if (route < 0) return route;
+    if (route) return chunk_store_host_hash(r, chunk_ids, chunk_hashes, st, ls);
+    return chunk_store_device(r, chunk_ids, chunk_hashes, st);
 }
 
 int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
@@ -604,31 +849,20 @@ int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
     if (!chunk_ids || !aligned4(chunk_ids) || !chunk_hashes || !ok)
         return fail(ENET_EINVAL, "chunk_fetch: NULL/misaligned chunk_ids, NULL hashes or ok");
     hipStream_t st = (hipStream_t)stream;
-    if (duplex_on()) {
-        enet::DuplexParams d = duplex_params(r);
-        d.chunk_ids = chunk_ids;
-        d.expect = chunk_hashes;
-        d.ok = ok;
-        return hip_status(enet::launch_duplex(enet::DK_CHUNK, true, d, st), "chunk_fetch duplex");
-    }
-    // 1) decrypt_with_key (CryptoManager.cpp:49-58)
-    enet::RecParams p = rec_params(r);
-    p.counters = reinterpret_cast<const uint32_t*>(chunk_ids);
-    p.counter_stride = 8;
-    if (int e = hip_status(enet::launch_records(enet::MODE_XOR, p, lanes_for(r), st),
-                           "chunk_fetch chacha"))
-        return e;
-    // 2) SHA-256(pt) == manifest.chunk_hash, else no plaintext (Node.cpp:1644-1655)
-    enet::ShaParams s{};
-    s.n = r->count;
-    s.in = r->out;
-    s.off = r->out_offsets;
-    s.expect = chunk_hashes;
-    s.ok = ok;
-    s.zero_on_fail = r->out;
-    s.order = r->order;
-    return hip_status(enet::launch_sha(s, st), "chunk_fetch sha verify");
+    LongSplit ls;
+    const int route = long_split(r, st, ls);
+    if (route < 0) return route;
+    if (route) return chunk_fetch_host_hash(r, chunk_ids, chunk_hashes, ok, st, ls);
+    return chunk_fetch_device(r, chunk_ids, chunk_hashes, ok, st);
 }
+
+int enet_set_host_hash_min(int64_t bytes) {
+    if (bytes < -1) return fail(ENET_EINVAL, "host_hash_min must be -1 (auto), 0 .. INT64_MAX");
+    g_hh_min.store(bytes, std::memory_order_relaxed);
+    return ENET_OK;
+}
+
+uint64_t enet_host_hash_batches(void) { return g_hh_batches.load(std::memory_order_relaxed); }
 
 int enet_wire_seal_batch(const enet_records* r, void* stream) {
     if (int e = check_records(r, true)) return e;

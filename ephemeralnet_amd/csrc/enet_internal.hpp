@@ -186,15 +186,26 @@ struct SegParams {
     const uint8_t* tag_in;
     uint8_t* tag_out;
     uint8_t* ok;
+    const uint32_t* order;     // nullable: the records to plan are order[0 .. n) (a subset)
     // scratch (stream-ordered, capi.cpp seg_begin)
     unsigned long long* hdr;   // count << 40 | tiles claimed
     SegEntry* entries;         // [entry_cap]
-    uint8_t* claimed;          // [n]
+    uint8_t* claimed;          // [index bound]: indexed by record
     uint32_t* partials;        // [tile_cap][8]
     uint32_t entry_cap, tile_cap;
     uint64_t long_min;
 };
 hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_blocks, hipStream_t s);
+// dst[width * list[k] + b] = src[width * k + b], k < m, b < width
+hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, uint8_t* dst, uint32_t width,
+                          hipStream_t s);
+
+// ---- long chunks: SHA-256 on host threads (chunk_hybrid.cpp)
+// digests[32 k] = SHA-256 of record list[k] of the batch at `base` (device memory, or host memory
+// the device maps), off = a HOST copy of its offsets; `ready` (nullable): an event the copies wait
+// for.  0 or -1 (err set).
+int host_hash_records(const uint8_t* base, const uint64_t* off, const uint32_t* list, uint32_t m,
+                      hipEvent_t ready, uint32_t threads, uint8_t* digests, std::string& err);
 
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len);
 uint32_t staging_variant();

@@ -105,7 +105,8 @@ __global__ __launch_bounds__(kSegThreads) void seg_plan_kernel(SegParams p) {
         if (threadIdx.x == 0) __hip_atomic_store(p.hdr, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
     }
-    for (uint32_t i = blockIdx.x * kSegThreads + threadIdx.x; i < p.n; i += gridDim.x * kSegThreads) {
+    for (uint32_t pos = blockIdx.x * kSegThreads + threadIdx.x; pos < p.n; pos += gridDim.x * kSegThreads) {
+        const uint32_t i = p.order ? p.order[pos] : pos;  // a subset of the batch (capi chunk paths)
         const uint64_t L = p.in_off[i + 1] - p.in_off[i];
         bool claim = L >= p.long_min && L < kSegMaxLen;
         uint32_t idx = 0, base = 0;
@@ -410,6 +411,24 @@ __global__ __launch_bounds__(kSegThreads) void seg_kernel(SegParams p) {
         }
         __syncthreads();  // the slab and red[] are reused by the next tile
     }
+}
+
+// dst[width * list[k] ..] = src[width * k ..] for k < m (results computed on the host for a subset
+// of the batch, e.g. the host-hashed digests of long chunks, capi.cpp)
+__global__ void scatter_kernel(const uint8_t* __restrict__ src, const uint32_t* __restrict__ list, uint32_t m,
+                               uint8_t* __restrict__ dst, uint32_t width) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (uint64_t)m * width) return;
+    const uint32_t k = (uint32_t)(t / width), b = (uint32_t)(t % width);
+    dst[(uint64_t)width * list[k] + b] = src[t];
+}
+
+hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, uint8_t* dst, uint32_t width,
+                          hipStream_t s) {
+    const uint64_t total = (uint64_t)m * width;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(scatter_kernel, dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, s, src, list, m, dst, width);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------- host side

@@ -172,7 +172,9 @@ ENET_API int enet_aead_hmac_open_batch(const enet_records* r, const uint8_t* tag
  * fetch: out_i = ChaCha20(key_i, nonce_i, LE32(chunk_ids[i][0..3]), in_i); ok[i] =
  *        SHA-256(out_i) == chunk_hashes[i]; on mismatch out_i is zeroed (no plaintext).
  * With chunk_ids given: one pass over HBM (hash and cipher together) for any lengths;
- * content-derived ids need the digest first (two passes). */
+ * content-derived ids need the digest first (two passes).  Long chunks (a stored file is one chunk
+ * of up to 32 MiB, Config.hpp:62) hash on host threads while the device ciphers them across every
+ * CU: see enet_set_host_hash_min -- such a call is synchronous. */
 ENET_API int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids,
                                     uint8_t* chunk_hashes, void* stream);
 ENET_API int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
@@ -373,6 +375,17 @@ ENET_API int enet_set_lanes_per_record(uint32_t lanes);
  * record; INT64_MAX: never).  Results are identical; tuning / test knob. */
 #define ENET_SEG_MIN (256u << 10)
 ENET_API int enet_set_seg_min(int64_t bytes);
+/* Chunk store / fetch: records of at least this many bytes (default ENET_HOST_HASH_MIN, and only
+ * while the host threads' chains finish before one GPU lane's would: sum(long) < ~60 x CPU budget x
+ * longest) have their SHA-256 computed on host threads (SHA-NI) while the device runs their
+ * ChaCha20 on the tiles -- SHA-256 of one message is one serial chain (~34 MB/s on a GPU lane,
+ * ~2.1 GB/s on a host core).  Such a call synchronises the stream: it reads the offsets first and
+ * returns when the batch is done.  -1 = auto; 0 .. INT64_MAX forces the threshold (INT64_MAX: never,
+ * every chain on the GPU).  Results are identical; tuning / test knob. */
+#define ENET_HOST_HASH_MIN (256u << 10)
+ENET_API int enet_set_host_hash_min(int64_t bytes);
+/* Chunk store / fetch batches that took the host-hash route in this process (tests / tuning). */
+ENET_API uint64_t enet_host_hash_batches(void);
 /* Batches that have taken the sequence-parallel path in this process (tests / tuning). */
 ENET_API uint64_t enet_seg_batches(void);
 /* Staging of uniform-length batches (all records the same length): 1 = register prefetch + LDS

@@ -20,6 +20,7 @@
 #   sessions   the reference's thread-per-session load (SessionManager.cpp:331-332, 337-388, 822):
 #              T session threads, each with ONE blocking frame in flight (queue_bench sync), device
 #              queue vs host engine vs auto, T = ${THREADS:-64 256 768}, two rounds
+#   chunks     long-chunk GPU tests (host-hash route, tiles) and the long-record side leg
 #   long-prof  the long-record side leg (1 x 32 MiB, 8 x 1 MiB; bench.py --long-only) plain and
 #              under a rocprofv3 kernel trace (per-kernel durations, launch gaps)
 # Round-wide evidence (kernel stats, PMC, side configs): tools/gpu_round.sh.
@@ -157,6 +158,13 @@ long-prof)
   cut -c1-600 $O/long.json
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_long -o long -- python bench.py --long-only > $O/long_prof.json 2> $O/long_prof.err
   find $O/prof_long -name "*kernel_stats.csv" -exec cat {} \; ;;
+chunks)
+  step pytest
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_chunks_long.py tests/test_gpu_segments.py -x -v --timeout 200 --timeout-method thread > $O/pytest_chunks.log 2>&1 || { tail -60 $O/pytest_chunks.log; exit 1; }
+  tail -3 $O/pytest_chunks.log
+  step long leg
+  timeout -k 10 240 python bench.py --long-only > $O/long.json 2> $O/long.err
+  cut -c1-1500 $O/long.json ;;
 *)
   echo "unknown recipe $R" >&2; exit 2 ;;
 esac
