@@ -82,6 +82,9 @@ def parse():
                     help="skip the long-record side leg (1 x 32 MiB, 8 x 1 MiB)")
     ap.add_argument("--long-only", action="store_true",
                     help="print only the long-record side leg (device-resident) and exit")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="host-resident keys: only the C5 share (no C2 e2e child) -- the one-GPU N = 8 "
+                         "rehearsal, where 8 ranks + 8 children already use the box's 16 GPU process slots")
     ap.add_argument("--no-host", action="store_true",
                     help="default line: skip the host-resident extra keys (C2 e2e, C5 per-GPU share)")
     ap.add_argument("--c5-chunk-mib", type=int, default=0,
@@ -1309,9 +1312,13 @@ def main():
     host = None
     if args.mode == "aead" and not args.no_host and (n, L) == (65536, 4096):
         import ephemeralnet_amd as E2
-        hc2 = host_c2_child(dev.index, n, L, args.chunk_mib, args.streams)
+        if args.no_e2e:
+            hc2 = {"gibs": 0.0, "seal_gibs": 0.0, "open_gibs": 0.0}
+        else:
+            hc2 = host_c2_child(dev.index, n, L, args.chunk_mib, args.streams)
         hc5 = c5_host_child_timed(world, rank, dev.index, red_dev, 65536, args.c5_chunk_mib, args.c5_streams)
-        hc2t = host_c2(dev.index, n, L, 3, args.chunk_mib, args.streams)  # this process: torch's runtime
+        hc2t = (host_c2(dev.index, n, L, 3, args.chunk_mib, args.streams) if not args.no_e2e  # torch's runtime
+                else {"gibs": 0.0, "host": {"mode": 3}})
         host = {"e2e_gibs": round(hc2["gibs"], 2), "e2e_seal_gibs": round(hc2["seal_gibs"], 2),
                 "e2e_open_gibs": round(hc2["open_gibs"], 2),
                 "e2e_is": "C2 (65 536 x 4 KiB) seal+open from and to pinned host memory, this rank",

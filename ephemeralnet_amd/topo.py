@@ -143,7 +143,10 @@ def rank_placement(local_rank: int, local_world: int) -> dict:
     CPUs within the affinity mask (the whole mask when the node is unknown or outside it) and
     its share of the CPU budget (min(mask, quota) / ranks, at least 1)."""
     allowed = allowed_cpus()
-    node = gpu_numa_node(local_rank)
+    # the rank's GPU: cuda:(local_rank mod GPUs), as bench.py binds it (ranks share the card when
+    # there are fewer GPUs than ranks -- the one-GPU rehearsal of N = 2 / 8)
+    fns = gpu_pci_functions()
+    node = gpu_numa_node(local_rank % len(fns) if fns else local_rank)
     cpus = sorted(set(node_cpus(node)) & set(allowed)) or allowed
     q = cgroup_quota_cpus()
     budget = min(len(allowed), q) if q else len(allowed)

@@ -121,6 +121,29 @@ def test_queues_16_threads_auto_policy_on_gpu(stress_bin):
     assert s["tx_host_flushes"] == s["tx_flushes"] == s["tx_frames"] and s["device_failures"] == 0, err
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("policy", ["auto", "device"])
+def test_queues_512_blocking_session_threads_on_gpu(stress_bin, policy):
+    """The reference's own session threading (SessionManager.cpp:331-332 one reader thread per
+    session; send() seals synchronously, :337-388; receive_loop opens one frame at a time, :822):
+    512 session threads, each with ONE blocking frame in flight, 20 frames each (a 64 KiB one and
+    the 1 MiB maximum payload among them), every 7th opened frame tampered, every 11th opened under
+    another session's key.  Every sealed frame is checked byte for byte against the host engine
+    (and 1 536 of them against the oracle).  Routing: AUTO serves every blocking frame on the
+    calling thread's host engine (profiles/r06_sessions_blocking.jsonl: 64-4 096 blocked threads
+    move 7-10 M frames/s there against 0.2-2.4 M through device passes); DEVICE batches the
+    blocked threads' frames into shared passes, no host flush."""
+    rc, s, sample, err = run(stress_bin, policy, threads=512, frames=20)
+    check_common(rc, s, sample, 512, 20)
+    assert s["device_failures"] == 0, err
+    if policy == "auto":
+        assert s["tx_host_flushes"] == s["tx_flushes"] == s["tx_frames"], s
+        assert s["rx_host_flushes"] == s["rx_flushes"] == s["rx_frames"], s
+    else:
+        assert s["tx_host_flushes"] == 0 and s["rx_host_flushes"] == 0, s
+        assert s["tx_flushes"] < s["tx_frames"] and s["rx_flushes"] < s["rx_frames"], s  # shared passes
+
+
 def run_async(stress_bin, policy, threads=8, frames=400):
     r = subprocess.run([stress_bin, "async", policy, str(threads), str(frames)], capture_output=True, text=True,
                        timeout=600)
