@@ -41,6 +41,15 @@ namespace {
 
 constexpr uint32_t kRun = 128;  // bytes per stage and record
 
+// one wave: its lanes' LDS writes are visible to its other lanes (DS ops of a wave execute in
+// issue order; a compiler barrier and a wave barrier suffice, no vmcnt drain)
+#define ENET_DX_WAVE_SYNC()               \
+    do {                                  \
+        asm volatile("" ::: "memory");    \
+        __builtin_amdgcn_wave_barrier();  \
+        asm volatile("" ::: "memory");    \
+    } while (0)
+
 // all waves: this wave's LDS traffic is done, then meet
 #define ENET_DX_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
@@ -72,6 +81,9 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
     __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kBuf];  // stage slabs
     __shared__ __attribute__((aligned(16))) uint8_t text[RPW * 32];  // tail slot bytes 128..159
     __shared__ uint32_t tmax_s;
+    // open: each record's output base and whole stages, for the line-wise plaintext stores
+    __shared__ uint64_t odst_s[OPEN ? RPW : 1];
+    __shared__ uint32_t ots_s[OPEN ? RPW : 1];
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -173,6 +185,10 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         const uint8_t* src = p.in + ib + (OPEN ? H : 0u);
         uint8_t* dst = p.out + ob + (OPEN ? 0u : H);
         const uint32_t off0 = OPEN ? H : 0u;  // offset of src inside the input record
+        if (OPEN) {
+            odst_s[rl] = reinterpret_cast<uint64_t>(dst);  // read after the first stage barrier
+            ots_s[rl] = Ts;
+        }
         uint32_t nw[3];
         if (OPEN && KIND == DK_FRAME && H) {  // nonce = the frame's first 12 bytes (SessionManager.cpp:815-822)
 #pragma unroll
@@ -216,8 +232,31 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 *reinterpret_cast<uint4*>(d + 16u * (k ^ msw)) =
                     make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
         };
+        // Open: every stage's plaintext is in the slab (for the hash lane); it is stored from there
+        // line by line one stage later (after the barrier that hands the slab to the hash lanes,
+        // which only read it; the cipher lanes rewrite it two stages on) -- instruction i serves
+        // the wave's records 8i .. 8i+7, eight lanes per record, each record's whole 128-byte run
+        // in one instruction.  Per-lane 16-byte stores wrote 64 records' lines in eight pieces
+        // each, and the pieces the L2 wrote back separately doubled the fetch's HBM writes
+        // (pmc_st_r05z.json: 2.03x the algorithmic write bytes; seal 1.42x).
+        auto store_stage = [&](uint32_t t) {
+            const uint32_t kk = lane & 7u;
+            const uint32_t wrow = 64u * (wave % kW);
+            const uint8_t* slab = ptb + (t & 1u) * kBuf;
+#pragma unroll 1
+            for (uint32_t i = 0; i < 8; ++i) {
+                const uint32_t o = 8u * i + (lane >> 3);
+                if (t < ots_s[wrow + o]) {
+                    const uint32_t sw = ((o >> 1) & 7u) ^ ((o & 1u) << 2);
+                    const uint4 v = *reinterpret_cast<const uint4*>(slab + (wrow + o) * kRun + 16u * kk);
+                    uint8_t* d = reinterpret_cast<uint8_t*>(odst_s[wrow + o]) + (uint64_t)kRun * t + 16u * (kk ^ sw);
+                    *reinterpret_cast<uint4*>(d) = v;
+                }
+            }
+        };
         if (Ts > 0) load_run(0);
         for (uint32_t s = 0; s < Tmax; ++s) {
+            if (OPEN && s > 0) store_stage(s - 1);
             if (s < Ts) {
                 uint32_t x[32];
 #pragma unroll
@@ -233,13 +272,17 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                     for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
                 }
                 if (KIND == DK_AEADH && !OPEN) poly_words(x, 8);
-                if (OPEN) put_run(pt, x);
-                uint4* o = reinterpret_cast<uint4*>(dst + (uint64_t)kRun * s);
+                if (OPEN) {
+                    put_run(pt, x);
+                } else {
+                    uint4* o = reinterpret_cast<uint4*>(dst + (uint64_t)kRun * s);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+                    for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
+                }
             }
             ENET_DX_BARRIER();  // stage s plaintext is in ptb[s & 1]
         }
+        if (OPEN && Tmax > 0) store_stage(Tmax - 1);
 
         // ---- ragged end
         const uint32_t tin = (OPEN && KIND == DK_FRAME) ? r + 32u : r;  // body-tail bytes read now

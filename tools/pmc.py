@@ -56,14 +56,15 @@ def main():
     ap.add_argument("--out", default="gpurun_out/pmc")
     ap.add_argument("--summary", default=None)
     ap.add_argument("--config", default=None, help="JSON dict recorded as the workload config")
-    ap.add_argument("--passes", default="default", choices=["default", "stall"])
+    ap.add_argument("--passes", default="default", choices=["default", "stall", "traffic"])
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
     os.makedirs(a.out, exist_ok=True)
     env = dict(os.environ, TMPDIR="/tmp")
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
-    for i, counters in enumerate(PASSES if a.passes == "default" else STALL_PASSES):
+    sets = {"default": PASSES, "stall": STALL_PASSES, "traffic": [["FETCH_SIZE"], ["WRITE_SIZE"]]}
+    for i, counters in enumerate(sets[a.passes]):
         tag = f"p{i}"
         rc = subprocess.run(["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d",
                              a.out, "-o", tag, "--", *cmd], env=env,
