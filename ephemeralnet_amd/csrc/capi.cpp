@@ -38,6 +38,19 @@ int hip_status(hipError_t e, const char* what) {
 
 bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3u) == 0; }
 
+// Kernel A/B knobs (ENET_NT_STORES, ENET_LOCKSTEP, ENET_STREAM, ENET_DUPLEX, ENET_COOP, ENET_LANES,
+// ENET_TARGET_LANES): read from the environment by the tools build only (build.py --tools ->
+// libenet_crypto_tools.so); the shipping library runs its defaults, and tests pick variants
+// through the enet_set_* calls.
+const char* tools_env(const char* name) {
+#ifdef ENET_TOOLS_BUILD
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 int check_records(const enet_records* r, bool need_keys) {
     if (!r) return fail(ENET_EINVAL, "records descriptor is NULL");
     if (r->count == 0) return ENET_OK;
@@ -75,17 +88,17 @@ enet::RecParams rec_params(const enet_records* r) {
     const bool dflt = p.coop == 1;
     p.coop_lines = dflt ? 1 : 0;
     static const int nt = [] {
-        const char* e = std::getenv("ENET_NT_STORES");
+        const char* e = tools_env("ENET_NT_STORES");
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.nt_stores = nt;
     static const int lock = [] {
-        const char* e = std::getenv("ENET_LOCKSTEP");
+        const char* e = tools_env("ENET_LOCKSTEP");
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.lockstep = dflt ? lock : 0;
     static const int strm = [] {
-        const char* e = std::getenv("ENET_STREAM");
+        const char* e = tools_env("ENET_STREAM");
         return (e && e[0] == '0') ? 0 : 1;
     }();
     p.stream = dflt ? strm : 0;
@@ -117,7 +130,7 @@ enet::RecParams rec_params(const enet_records* r) {
 // records kernel) instead.
 bool duplex_on() {
     static const bool on = [] {
-        const char* e = std::getenv("ENET_DUPLEX");
+        const char* e = tools_env("ENET_DUPLEX");
         return !(e && e[0] == '0');
     }();
     return on && enet::staging_variant() != 0;
@@ -541,7 +554,7 @@ int duplex_split_mode() { return g_duplex_split.load(std::memory_order_relaxed);
 // override (tests).  (3, the LDS-DMA four-waves-per-SIMD variant, was retired in round 6.)
 uint32_t staging_variant() {
     static const uint32_t env = [] {
-        const char* s = std::getenv("ENET_COOP");
+        const char* s = tools_env("ENET_COOP");
         return s ? (uint32_t)std::strtoul(s, nullptr, 10) + 1u : 0u;
     }();
     if (uint32_t f = g_staging.load(std::memory_order_relaxed)) return f - 1u;
@@ -556,11 +569,11 @@ uint32_t staging_variant() {
 // value (tuning / tests).
 uint32_t choose_lanes(uint32_t n, uint64_t total_bytes, uint32_t max_len) {
     static const uint32_t forced = [] {
-        const char* s = std::getenv("ENET_LANES");
+        const char* s = tools_env("ENET_LANES");
         return s ? (uint32_t)std::strtoul(s, nullptr, 10) : 0u;
     }();
     static const uint64_t target = [] {
-        const char* s = std::getenv("ENET_TARGET_LANES");
+        const char* s = tools_env("ENET_TARGET_LANES");
         return s ? (uint64_t)std::strtoull(s, nullptr, 10) : 131072ull;
     }();
     if (uint32_t f = g_forced_lanes.load(std::memory_order_relaxed)) return f;

@@ -555,16 +555,22 @@ hipError_t launch_duplex(int kind, bool open, const DuplexParams& p, hipStream_t
             return launch_duplex_split(kind, open, q, s);
         }
     }
+    // A/B knobs, compiled into kernel objects built with -DENET_TOOLS_BUILD only (build.py --tools
+    // --probes)
+#ifdef ENET_TOOLS_BUILD
     static const int prio_env = [] {
         const char* e = std::getenv("ENET_DUPLEX_PRIO");
         return e ? (int)std::strtol(e, nullptr, 10) : 0;
     }();
-    DuplexParams q = p;
-    q.prio = prio_env;
     static const int rpw_env = [] {
         const char* e = std::getenv("ENET_DUPLEX_RPW");
         return e ? (int)std::strtol(e, nullptr, 10) : 0;
     }();
+#else
+    constexpr int prio_env = 0, rpw_env = 0;
+#endif
+    DuplexParams q = p;
+    q.prio = prio_env;
     // Mixed lengths: 64-record workgroups, so the few long records (a workgroup lasts as long as
     // its longest record's serial hash) occupy few SIMDs and the rest of the chip keeps pulling
     // short workgroups (C5 device-resident: 88 -> 138 GiB/s).  Uniform batches: 256-record
