@@ -383,7 +383,9 @@ int long_split(const enet_records* r, hipStream_t st, LongSplit& ls) {
     const int64_t f = g_hh_min.load(std::memory_order_relaxed);
     if (f == INT64_MAX || r->order) return 0;  // a caller-ordered subset keeps its own schedule
     const uint64_t lmin = f >= 0 ? (uint64_t)f : kHostHashMin;
-    if (f < 0 && r->max_len_hint && r->max_len_hint < lmin) return 0;  // hint: nothing that long
+    // only when the caller's hint says a record may be that long: the route reads the offsets
+    // back (a stream synchronisation), which a batch of short chunks must not pay
+    if (r->max_len_hint < lmin || r->max_len_hint == 0) return 0;
     const uint32_t n = r->count;
     ls.in_off.resize(n + 1);
     ls.out_off.resize(n + 1);
@@ -848,10 +850,14 @@ int enet_chunk_store_batch(const enet_records* r, const uint8_t* chunk_ids, uint
         return fail(ENET_EINVAL, "chunk_store: chunk_hashes NULL or misaligned");
     if (chunk_ids && !aligned4(chunk_ids)) return fail(ENET_EINVAL, "chunk_store: chunk_ids misaligned");
     hipStream_t st = (hipStream_t)stream;
-    LongSplit ls;
-    const int route = long_split(r, st, ls);
-    if (route < 0) return route;
-    if (route) return chunk_store_host_hash(r, chunk_ids, chunk_hashes, st, ls);
+    try {  // the host route allocates and starts threads: nothing may escape the C ABI
+        LongSplit ls;
+        const int route = long_split(r, st, ls);
+        if (route < 0) return route;
+        if (route) return chunk_store_host_hash(r, chunk_ids, chunk_hashes, st, ls);
+    } catch (const std::exception& e) {
+        return fail(ENET_EHIP, (std::string("chunk_store: ") + e.what()).c_str());
+    }
     return chunk_store_device(r, chunk_ids, chunk_hashes, st);
 }
 
@@ -862,10 +868,14 @@ int enet_chunk_fetch_batch(const enet_records* r, const uint8_t* chunk_ids,
     if (!chunk_ids || !aligned4(chunk_ids) || !chunk_hashes || !ok)
         return fail(ENET_EINVAL, "chunk_fetch: NULL/misaligned chunk_ids, NULL hashes or ok");
     hipStream_t st = (hipStream_t)stream;
-    LongSplit ls;
-    const int route = long_split(r, st, ls);
-    if (route < 0) return route;
-    if (route) return chunk_fetch_host_hash(r, chunk_ids, chunk_hashes, ok, st, ls);
+    try {
+        LongSplit ls;
+        const int route = long_split(r, st, ls);
+        if (route < 0) return route;
+        if (route) return chunk_fetch_host_hash(r, chunk_ids, chunk_hashes, ok, st, ls);
+    } catch (const std::exception& e) {
+        return fail(ENET_EHIP, (std::string("chunk_fetch: ") + e.what()).c_str());
+    }
     return chunk_fetch_device(r, chunk_ids, chunk_hashes, ok, st);
 }
 

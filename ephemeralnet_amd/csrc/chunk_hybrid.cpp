@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -111,6 +112,11 @@ int host_hash_records(const uint8_t* base, const uint64_t* off, const uint32_t* 
                         (base - static_cast<const uint8_t*>(a.devicePointer ? a.devicePointer : a.hostPointer));
         (void)hipGetLastError();  // an unregistered pointer leaves an error behind
     }
+    // host memory is read by the CPU directly: the producing stream's work must be done first
+    if (host_base && ready && hipEventSynchronize(ready) != hipSuccess) {
+        err = "host hash: hipEventSynchronize failed";
+        return -1;
+    }
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) {
         err = "host hash: hipGetDevice failed";
@@ -147,7 +153,13 @@ int host_hash_records(const uint8_t* base, const uint64_t* off, const uint32_t* 
     };
     std::vector<std::thread> pool;
     pool.reserve(T - 1);
-    for (uint32_t t = 1; t < T; ++t) pool.emplace_back(run, t);
+    for (uint32_t t = 1; t < T; ++t) {
+        try {
+            pool.emplace_back(run, t);
+        } catch (const std::system_error&) {
+            break;  // fewer threads: the started ones and this one take the rest of the list
+        }
+    }
     run(0);
     for (auto& th : pool) th.join();
     if (failed) {

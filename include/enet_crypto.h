@@ -379,8 +379,9 @@ ENET_API int enet_set_seg_min(int64_t bytes);
  * while the host threads' chains finish before one GPU lane's would: sum(long) < ~60 x CPU budget x
  * longest) have their SHA-256 computed on host threads (SHA-NI) while the device runs their
  * ChaCha20 on the tiles -- SHA-256 of one message is one serial chain (~34 MB/s on a GPU lane,
- * ~2.1 GB/s on a host core).  Such a call synchronises the stream: it reads the offsets first and
- * returns when the batch is done.  -1 = auto; 0 .. INT64_MAX forces the threshold (INT64_MAX: never,
+ * ~2.1 GB/s on a host core).  Taken only when the batch's max_len_hint is at least the threshold;
+ * such a call synchronises the stream: it reads the offsets first and returns when the batch is
+ * done.  -1 = auto; 0 .. INT64_MAX forces the threshold (INT64_MAX: never,
  * every chain on the GPU).  Results are identical; tuning / test knob. */
 #define ENET_HOST_HASH_MIN (256u << 10)
 ENET_API int enet_set_host_hash_min(int64_t bytes);

@@ -187,3 +187,35 @@ def test_forced_threshold_small_chunks(enet):
                                                               oracle.derive_counter(ids[i])), i
         assert bh[offs[i]:offs[i + 1]] == items[i], i
     assert ok == [1] * n
+
+
+def test_long_chunks_in_host_mapped_memory(enet):
+    """Arenas in pinned host memory the device maps (what the host-batch runtime's zero-copy mode
+    and enet_host_alloc callers hand the C ABI): the host threads hash the long chunks where they
+    lie -- on fetch only after the decrypt kernel has finished writing them -- and the bytes match
+    the device-memory run."""
+    import torch
+    lens = [3 * MiB + 5, 700, (256 << 10) + 64]
+    n = len(lens)
+    b, items, keys, nonces = make(enet, lens, 7300)
+    ids = ids_for(n, 17)
+    ct_dev, hh_dev = store(enet, b, ids)
+    pin_in = b.arena.cpu().pin_memory()
+    pin_ct = torch.full_like(pin_in, 0x55).pin_memory()
+    hashes = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    import dataclasses
+    bh = dataclasses.replace(b, arena=pin_in)
+    before = enet.host_hash_batches()
+    enet.chunk_store(bh, pin_ct, hashes, chunk_ids=dev(b"".join(ids)))
+    torch.cuda.synchronize()
+    assert enet.host_hash_batches() == before + 1
+    assert host(hashes) == hh_dev and pin_ct.numpy().tobytes() == host(ct_dev)
+    back = torch.full_like(pin_in, 0xAA).pin_memory()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.chunk_fetch(dataclasses.replace(b, arena=pin_ct), back, dev(b"".join(ids)), dev(hh_dev), ok)
+    torch.cuda.synchronize()
+    assert ok.cpu().tolist() == [1] * n
+    offs = b.offsets.cpu().tolist()
+    bb = back.numpy().tobytes()
+    for i in range(n):
+        assert bb[offs[i]:offs[i + 1]] == items[i], i
