@@ -81,9 +81,12 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
     __shared__ __attribute__((aligned(16))) uint8_t ptb[2 * kBuf];  // stage slabs
     __shared__ __attribute__((aligned(16))) uint8_t text[RPW * 32];  // tail slot bytes 128..159
     __shared__ uint32_t tmax_s;
-    // open: each record's output base and whole stages, for the line-wise plaintext stores
-    __shared__ uint64_t odst_s[OPEN ? RPW : 1];
-    __shared__ uint32_t ots_s[OPEN ? RPW : 1];
+    // chunk fetch: each record's output base and whole stages, for the line-wise plaintext stores
+    // (the frame and AEAD+HMAC opens keep per-lane stores: at the 128-VGPR cap the line-wise form
+    // spilled there and cost C3 wire open 4 %, 1 904 -> 1 981 us, r06 prof_c3w)
+    constexpr bool kLines = OPEN && KIND == DK_CHUNK;
+    __shared__ uint64_t odst_s[kLines ? RPW : 1];
+    __shared__ uint32_t ots_s[kLines ? RPW : 1];
 
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
@@ -185,7 +188,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         const uint8_t* src = p.in + ib + (OPEN ? H : 0u);
         uint8_t* dst = p.out + ob + (OPEN ? 0u : H);
         const uint32_t off0 = OPEN ? H : 0u;  // offset of src inside the input record
-        if (OPEN) {
+        if (kLines) {
             odst_s[rl] = reinterpret_cast<uint64_t>(dst);  // read after the first stage barrier
             ots_s[rl] = Ts;
         }
@@ -232,7 +235,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                 *reinterpret_cast<uint4*>(d + 16u * (k ^ msw)) =
                     make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
         };
-        // Open: every stage's plaintext is in the slab (for the hash lane); it is stored from there
+        // Chunk fetch: every stage's plaintext is in the slab (for the hash lane); it is stored from there
         // line by line one stage later (after the barrier that hands the slab to the hash lanes,
         // which only read it; the cipher lanes rewrite it two stages on) -- instruction i serves
         // the wave's records 8i .. 8i+7, eight lanes per record, each record's whole 128-byte run
@@ -256,7 +259,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
         };
         if (Ts > 0) load_run(0);
         for (uint32_t s = 0; s < Tmax; ++s) {
-            if (OPEN && s > 0) store_stage(s - 1);
+            if (kLines && s > 0) store_stage(s - 1);
             if (s < Ts) {
                 uint32_t x[32];
 #pragma unroll
@@ -272,9 +275,8 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
                     for (int i = 0; i < 16; ++i) { x[i] ^= ka[i]; x[16 + i] ^= kb[i]; }
                 }
                 if (KIND == DK_AEADH && !OPEN) poly_words(x, 8);
-                if (OPEN) {
-                    put_run(pt, x);
-                } else {
+                if (OPEN) put_run(pt, x);
+                if (!kLines) {
                     uint4* o = reinterpret_cast<uint4*>(dst + (uint64_t)kRun * s);
 #pragma unroll
                     for (int i = 0; i < 8; ++i) o[i] = make_uint4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
@@ -282,7 +284,7 @@ __device__ __forceinline__ void duplex_body(const DuplexParams& p) {
             }
             ENET_DX_BARRIER();  // stage s plaintext is in ptb[s & 1]
         }
-        if (OPEN && Tmax > 0) store_stage(Tmax - 1);
+        if (kLines && Tmax > 0) store_stage(Tmax - 1);
 
         // ---- ragged end
         const uint32_t tin = (OPEN && KIND == DK_FRAME) ? r + 32u : r;  // body-tail bytes read now
