@@ -45,7 +45,7 @@ METRICS = {  # the headline is `aead`; the others are SURVEY 8d/8f side measurem
     "wire": "GiB/s session wire frames seal+open (device-resident)",
     "store": "GiB/s chunk store+fetch pipeline, SHA-256 + ChaCha20 (device-resident)",
 }
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r05z.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_r06.json")
 VALU_CEILING_FILE = os.path.join(ROOT, "profiles", "valu_ceiling_r02.json")
 
 
