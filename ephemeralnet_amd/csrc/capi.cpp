@@ -266,6 +266,25 @@ int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t
                 uint32_t index_n = 0) {
     uint64_t long_min = 0;
     SegRun sr;
+    // XOR over a batch the hints call uniform and long: one launch of tile workgroups, nothing
+    // else (a record that is not as hinted is run whole by its tile-0 workgroup)
+    if (mode == enet::MODE_XOR && !r->order && seg_wanted(r, long_min) && r->max_len_hint >= long_min &&
+        r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint) {
+        enet::SegParams q{};
+        q.mode = mode;
+        q.n = r->count;
+        q.in_off = p.in_off;
+        q.out_off = p.out_off;
+        q.in = p.in;
+        q.out = p.out;
+        q.keys = p.keys;
+        q.key_stride = p.key_stride;
+        q.nonces = p.nonces;
+        q.counters = p.counters;
+        q.counter_stride = p.counter_stride;
+        g_seg_batches.fetch_add(1, std::memory_order_relaxed);
+        return hip_status(enet::launch_seg_uniform_xor(q, r->max_len_hint, st), what);
+    }
     if (mode <= enet::MODE_OPEN && seg_wanted(r, long_min)) {
         if (int e = seg_begin(mode, r, p, long_min, st, sr, index_n ? index_n : r->count)) {
             seg_end(sr, st);

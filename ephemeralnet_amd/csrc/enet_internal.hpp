@@ -196,6 +196,10 @@ struct SegParams {
     uint64_t long_min;
 };
 hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_blocks, hipStream_t s);
+// ChaCha20 over a batch whose hints say every record is L >= kSegMin bytes: one launch of n *
+// ceil(L / 64 KiB) tile workgroups; records whose real length differs are run whole by their
+// tile-0 workgroup (p.n, offsets, arenas, keys, nonces, counters used; no scratch)
+hipError_t launch_seg_uniform_xor(const SegParams& p, uint64_t L, hipStream_t s);
 // dst[width * list[k] + b] = src[width * k + b], k < m, b < width
 hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, uint8_t* dst, uint32_t width,
                           hipStream_t s);

@@ -413,6 +413,130 @@ __global__ __launch_bounds__(kSegThreads) void seg_kernel(SegParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------- uniform XOR
+// ChaCha20 (XOR mode) over a batch whose hints say every record is L >= ENET_SEG_MIN bytes: ONE
+// launch, no plan and no record-engine pass.  Workgroup t serves tile t % T of record t / T
+// (T = ceil(L / 64 KiB)); every workgroup checks its record against the hint, and a record whose
+// real length differs is run whole by the workgroup of its tile 0, tile after tile (a wrong hint
+// costs speed, never bytes).  The three-launch path (plan, tiles, record engine) cost ~4 us per
+// launch whatever the launch does (profiles/r06b_long_kernel_stats.csv).
+
+// One tile of a record in XOR mode: lane j owns blocks [tb0 + 4j, +4) clipped to the record.
+__device__ __forceinline__ void xor_tile(const uint8_t* src, uint8_t* dst, uint64_t L, uint32_t tb0,
+                                         uint32_t ctr0, const ChachaRecord& R, uint8_t* slab) {
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    const uint32_t j = threadIdx.x;
+    const uint32_t nb = (uint32_t)((L + 63) >> 6);
+    const uint32_t tb1 = min(tb0 + kTileBlocks, nb);
+    const uint32_t c0 = min(tb0 + kSegBPL * j, tb1), c1 = min(c0 + kSegBPL, tb1);
+    const bool whole = (uint64_t)(tb0 + kTileBlocks) * 64ull <= L;  // uniform over the workgroup
+    if (whole) {
+        const uint32_t kk = lane & 7u;
+        const uint32_t msw = slab_sw(lane);
+        uint8_t* wslab = slab + wbase * kRun;
+        uint8_t* myrun = slab + threadIdx.x * kRun;
+        const uint8_t* ib = src + 64ull * tb0;
+        uint8_t* ob = dst + 64ull * tb0;
+        const bool nt = ((reinterpret_cast<uintptr_t>(ob)) & 63u) == 0;
+        uint32_t offs[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t o = 8u * i + (lane >> 3);
+            offs[i] = 64u * kSegBPL * (wbase + o) + 16u * (kk ^ slab_sw(o));
+        }
+        uint32_t pf[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint4 v = *reinterpret_cast<const uint4*>(ib + offs[i]);
+            pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) =
+                    make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+            ENET_WAVE_LDS_SYNC();
+            uint32_t w2[32];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint4 v = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                w2[4 * k] = v.x; w2[4 * k + 1] = v.y; w2[4 * k + 2] = v.z; w2[4 * k + 3] = v.w;
+            }
+            if (st == 0) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ib + offs[i] + kRun);
+                    pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
+                }
+            }
+            const uint32_t cb = ctr0 + c0 + 2u * st;  // u32 wrap (ChaCha20.cpp:110)
+            uint32_t ka[16], kb[16];
+            chacha_block2(R, cb, cb + 1u, ka, kb);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                    make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+            ENET_WAVE_LDS_SYNC();
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint4 v = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                store_stream(ob + offs[i] + kRun * st, v, nt);
+            }
+        }
+    } else {
+        for (uint32_t c = c0; c < c1; ++c) {
+            const uint64_t pos = 64ull * c;
+            const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
+            uint32_t w[16];
+            load_block(src + pos, nbytes, w, pos + nbytes >= 16);
+            uint32_t o[16];
+            chacha_block(R, ctr0 + c, o);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] ^= w[i];
+            store_block(dst + pos, nbytes, o);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSegThreads) void seg_uniform_xor_kernel(SegParams p, uint64_t L, uint32_t T) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kSegThreads * kRun];
+    const uint32_t rec = blockIdx.x / T, tr = blockIdx.x % T;
+    const uint64_t ioff = p.in_off[rec];
+    const uint64_t Lr = p.in_off[rec + 1] - ioff;
+    const bool as_hinted = p.in_off[rec + 1] >= ioff && Lr == L;
+    if (!as_hinted && tr != 0) return;  // the record's tile-0 workgroup runs it whole
+    uint32_t kw[8], nw[3];
+    {
+        const uint32_t* kp = reinterpret_cast<const uint32_t*>(p.keys + (size_t)p.key_stride * rec);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kw[i] = kp[i];
+        const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * rec);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) nw[i] = np[i];
+    }
+    ChachaRecord R;
+    chacha_record_init(R, kw, nw);
+    const uint32_t ctr0 = seg_counter(p, rec);
+    const uint8_t* src = p.in + ioff;
+    uint8_t* dst = p.out + p.out_off[rec];
+    if (as_hinted) {
+        xor_tile(src, dst, L, tr * kTileBlocks, ctr0, R, slab);
+        return;
+    }
+    // the hint was wrong for this record: all of it here (empty or disordered offsets: nothing)
+    if (p.in_off[rec + 1] < ioff) return;
+    const uint64_t ntile = (Lr + kTileBytes - 1) / kTileBytes;
+    for (uint64_t t = 0; t < ntile; ++t) {
+        xor_tile(src, dst, Lr, (uint32_t)(t * kTileBlocks), ctr0, R, slab);
+        __syncthreads();  // the slab is reused by the next tile
+    }
+}
+
 // dst[width * list[k] ..] = src[width * k ..] for k < m (results computed on the host for a subset
 // of the batch, e.g. the host-hashed digests of long chunks, capi.cpp)
 __global__ void scatter_kernel(const uint8_t* __restrict__ src, const uint32_t* __restrict__ list, uint32_t m,
@@ -432,6 +556,15 @@ hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, 
 }
 
 // ---------------------------------------------------------------------------------- host side
+hipError_t launch_seg_uniform_xor(const SegParams& p, uint64_t L, hipStream_t s) {
+    const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
+    const uint64_t blocks = (uint64_t)p.n * T;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFFull || T > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(seg_uniform_xor_kernel, dim3((uint32_t)blocks), dim3(kSegThreads), 0, s, p, L, (uint32_t)T);
+    return hipGetLastError();
+}
+
 hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_blocks, hipStream_t s) {
     if (plan_blocks > 1) {
         if (hipError_t e = hipMemsetAsync(p.hdr, 0, sizeof(unsigned long long), s)) return e;

@@ -206,3 +206,31 @@ def test_seg_never_and_auto_agree(enet):
         outs.append((host(ct), host(tags)))
     enet.set_seg_min(-1)
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("lens", [[300 << 10] * 4, [300 << 10, 100, (600 << 10) + 7, 0, 300 << 10, 65536 + 1]])
+def test_seg_uniform_xor_one_launch_and_lying_hints(enet, lens):
+    """ChaCha20 over a batch the hints call uniform (n x 300 KiB): one launch of tile workgroups,
+    no plan, no record-engine pass.  The second shape lies -- records of 100 B, 600 KiB + 7, 0 and
+    64 KiB + 1 under a 300 KiB hint -- and each such record is run whole by its tile-0 workgroup:
+    the bytes are the oracle's either way.  Counters near the u32 wrap; in place too."""
+    import torch
+    n = len(lens)
+    b, items, keys, nonces = make(enet, lens, 9300 + len(lens))
+    hinted = enet.Batch(b.arena, b.offsets, b.keys, b.nonces, total_bytes_hint=n * (300 << 10),
+                        max_len_hint=300 << 10)
+    ctr = np.array([0xFFFFFFFF - 37 * i for i in range(n)], dtype=np.uint32)
+    counters = torch.tensor(ctr.view(np.int32)).cuda()
+    offs = b.offsets.cpu().tolist()
+    for inplace in (False, True):
+        out = b.arena.clone() if inplace else torch.zeros_like(b.arena)
+        src = enet.Batch(out, b.offsets, b.keys, b.nonces, total_bytes_hint=n * (300 << 10),
+                         max_len_hint=300 << 10) if inplace else hinted
+        before = enet.seg_batches()
+        enet.chacha20_xor(src, out, counters=counters)
+        torch.cuda.synchronize()
+        assert enet.seg_batches() == before + 1
+        oh = host(out)
+        for i in range(n):
+            want = oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i]))
+            assert oh[offs[i]:offs[i + 1]] == want, f"record {i} (len {lens[i]}, in place {inplace})"
