@@ -346,7 +346,9 @@ __global__ __launch_bounds__(kSegThreads) void seg_kernel(SegParams p) {
             const uint32_t tile_end = na + min(4u * tb1, nct) + (last_tile ? 1u : 0u);
             uint32_t l[5];
             h32_to_limbs(h, l);
+#ifndef ENET_SEG_PROBE_NO_SCALE  // timing probes (hand-built libraries only; wrong tags)
             if (c1 > c0 || (tr == 0 && j == 0)) pscale(l, tile_end - lane_end, E.pw, min(E.nbits, 14u));
+#endif
             wg_sum(l, red);
             // Publish the tile's partial; the record's last tile to arrive finishes the record.
             // Hand-off without an L2 write-back (MI355X_MICROARCH.md, inter-workgroup visibility,
@@ -363,6 +365,9 @@ __global__ __launch_bounds__(kSegThreads) void seg_kernel(SegParams p) {
                 last_flag = prev + 1 == E.ntiles ? 1u : 0u;
             }
             __syncthreads();
+#ifdef ENET_SEG_PROBE_NO_TAIL
+            last_flag = 0;
+#endif
             if (last_flag) {
                 const uint32_t nt = E.ntiles;
                 const uint32_t K = na + nct + 1;
