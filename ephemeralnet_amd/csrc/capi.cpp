@@ -205,6 +205,78 @@ struct SegRun {
     const uint8_t* claimed = nullptr;
 };
 
+// Per-stream arrival counters of the one-launch AEAD path (segments.hip seg_uniform_aead_kernel):
+// zeroed when allocated, reset by each record's last arriver, so they are zero whenever a launch
+// on that stream starts (launches on one stream run in order).  Grown on demand, stream-ordered.
+struct Arrivals {
+    uint32_t* ptr = nullptr;
+    uint32_t cap = 0;
+};
+
+int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<int, hipStream_t>, Arrivals>> table;
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return hip_status(e, "aead tiles: hipGetDevice");
+    std::lock_guard<std::mutex> lk(mu);
+    Arrivals* a = nullptr;
+    for (auto& kv : table)
+        if (kv.first.first == dev && kv.first.second == st) a = &kv.second;
+    if (!a) {
+        table.push_back({{dev, st}, Arrivals{}});
+        a = &table.back().second;
+    }
+    if (a->cap < n) {
+        hipMemPool_t pool = seg_pool();
+        if (!pool) return fail(ENET_EHIP, "aead tiles: no memory pool for the current device");
+        const uint32_t cap = std::max<uint32_t>(n, 1024u);
+        void* mem = nullptr;
+        if (hipError_t e = hipMallocFromPoolAsync(&mem, 4ull * cap, pool, st)) return hip_status(e, "aead tiles: counters");
+        if (hipError_t e = hipMemsetAsync(mem, 0, 4ull * cap, st)) return hip_status(e, "aead tiles: counters");
+        if (a->ptr) (void)hipFreeAsync(a->ptr, st);
+        a->ptr = static_cast<uint32_t*>(mem);
+        a->cap = cap;
+    }
+    out = a->ptr;
+    return ENET_OK;
+}
+
+// RFC 8439 seal / open over a batch the hints call uniform and long: one launch
+int run_uniform_aead(int mode, const enet_records* r, const enet::RecParams& p, hipStream_t st, const char* what) {
+    const uint64_t L = r->max_len_hint;
+    const uint64_t T = (L + enet::kSegTileBytes - 1) / enet::kSegTileBytes;
+    const uint64_t tiles = (uint64_t)r->count * T;
+    uint32_t* arr = nullptr;
+    const uint64_t words = (uint64_t)r->count * enet::seg_uniform_arrival_words();
+    if (words > UINT32_MAX) return fail(ENET_EINVAL, "aead tiles: too many records for one launch");
+    if (int e = arrivals_for(st, (uint32_t)words, arr)) return e;
+    hipMemPool_t pool = seg_pool();
+    if (!pool) return fail(ENET_EHIP, "aead tiles: no memory pool for the current device");
+    const size_t bytes = (size_t)tiles * 32;
+    void* mem = nullptr;
+    if (hipError_t e = hipMallocFromPoolAsync(&mem, bytes, pool, st)) return hip_status(e, "aead tiles: scratch");
+    enet::SegParams q{};
+    q.mode = mode;
+    q.n = r->count;
+    q.in_off = p.in_off;
+    q.out_off = p.out_off;
+    q.in = p.in;
+    q.out = p.out;
+    q.keys = p.keys;
+    q.key_stride = p.key_stride;
+    q.nonces = p.nonces;
+    q.aad = p.aad;
+    q.aad_off = p.aad_off;
+    q.tag_in = p.tag_in;
+    q.tag_out = p.tag_out;
+    q.ok = p.ok;
+    q.partials = static_cast<uint32_t*>(mem);
+    g_seg_batches.fetch_add(1, std::memory_order_relaxed);
+    const int rc = hip_status(enet::launch_seg_uniform_aead(q, L, arr, st), what);
+    (void)hipFreeAsync(mem, st);
+    return rc;
+}
+
 // Plan + tile kernels for the batch's long records; sr.claimed marks them for the record engine.
 // index_n: one past the largest record index (r->count unless r->order names a subset).
 int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long_min, hipStream_t st,
@@ -285,6 +357,12 @@ int run_records(int mode, const enet_records* r, enet::RecParams& p, hipStream_t
         g_seg_batches.fetch_add(1, std::memory_order_relaxed);
         return hip_status(enet::launch_seg_uniform_xor(q, r->max_len_hint, st), what);
     }
+    // AEAD over such a batch: one launch too (the last tile of each record to arrive combines,
+    // and zeroes a failed open itself)
+    if ((mode == enet::MODE_SEAL || mode == enet::MODE_OPEN) && !r->order && seg_wanted(r, long_min) &&
+        r->max_len_hint >= long_min && r->total_bytes_hint == (uint64_t)r->count * r->max_len_hint &&
+        (uint64_t)r->count * ((r->max_len_hint + enet::kSegTileBytes - 1) / enet::kSegTileBytes) < 0x7FFFFFFFull)
+        return run_uniform_aead(mode, r, p, st, what);
     if (mode <= enet::MODE_OPEN && seg_wanted(r, long_min)) {
         if (int e = seg_begin(mode, r, p, long_min, st, sr, index_n ? index_n : r->count)) {
             seg_end(sr, st);

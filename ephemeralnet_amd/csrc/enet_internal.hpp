@@ -200,6 +200,11 @@ hipError_t launch_seg(const SegParams& p, uint32_t plan_blocks, uint32_t tile_bl
 // ceil(L / 64 KiB) tile workgroups; records whose real length differs are run whole by their
 // tile-0 workgroup (p.n, offsets, arenas, keys, nonces, counters used; no scratch)
 hipError_t launch_seg_uniform_xor(const SegParams& p, uint64_t L, hipStream_t s);
+// RFC 8439 seal / open over such a batch, one launch (segments.hip seg_uniform_aead_kernel):
+// p.partials [n * T][8] scratch; arrivals [n][seg_uniform_arrival_words()] zero at launch (reset
+// by the kernel)
+hipError_t launch_seg_uniform_aead(const SegParams& p, uint64_t L, uint32_t* arrivals, hipStream_t s);
+uint32_t seg_uniform_arrival_words();
 // dst[width * list[k] + b] = src[width * k + b], k < m, b < width
 hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, uint8_t* dst, uint32_t width,
                           hipStream_t s);

@@ -64,6 +64,9 @@ __device__ __forceinline__ void pscale(uint32_t l[5], uint32_t e, const uint32_t
     }
 }
 
+// l <- l * m (26-bit limbs)
+__device__ __forceinline__ void pmul_by(uint32_t l[5], const uint32_t m[5]) { pmul(l, pmul_make(m)); }
+
 // Sum of the workgroup's 256 accumulators (limbs < 2^27) into thread 0's l (limbs < 2^27)
 __device__ __forceinline__ void wg_sum(uint32_t l[5], uint32_t* red /* [4][5] shared */) {
 #pragma unroll
@@ -542,6 +545,596 @@ __global__ __launch_bounds__(kSegThreads) void seg_uniform_xor_kernel(SegParams 
     }
 }
 
+// ---------------------------------------------------------------------------------- uniform AEAD
+// RFC 8439 seal / open over a batch whose hints say every record is L >= ENET_SEG_MIN bytes: ONE
+// launch (the three-launch path spent ~12 of its ~51 us per 32 MiB record in the plan and the
+// record-engine pass, profiles/r06i_seg_probes.txt).  Workgroup t serves tile t % T of record
+// t / T with four data waves and a fifth "power" wave:
+//   * the power wave derives the record's one-time key (block 0) and r^(2^k), k <= 12, into LDS
+//     (the data waves load and run their first keystream meanwhile, and wait at one barrier before
+//     their first Poly1305 step); in the record's tile-0 workgroup it then goes on squaring --
+//     r^(2^k) up to what the combine needs, and r^R for the last tile -- into the record's global
+//     table, published before that workgroup's arrival;
+//   * tiles publish their partial write-through and take an arrival ticket (as seg_kernel); the
+//     last to arrive combines: Horner over q right-aligned tiles per lane in r^4096, a shuffle / LDS
+//     tree whose level multipliers are table entries, then h = Q r^R + P_last;
+//   * open: every tile stores its plaintext write-through (sc1) and drains it before arriving, so
+//     the last arriver can zero a failed record itself (no later pass needed);
+//   * the arrival counters are per-stream state, zero when the launch starts (capi.cpp) and reset
+//     by each record's last arriver;
+//   * a record whose real length differs from the hint is run whole by its tile-0 workgroup, tile
+//     after tile, its partials combined in that workgroup (a wrong hint costs speed, never bytes).
+constexpr uint32_t kUThreads = kSegThreads + 64;   // four data waves + the power wave
+constexpr uint32_t kUPow = 44;                      // LDS table entries r^(2^k), k < 44
+// Arrival counters per record: a top counter and kUGroups group counters, each on its own 128-byte
+// line.  Tile t arrives at group t mod kUGroups; a group's last arriver arrives at the top counter.
+// (One counter per record took all of a 32 MiB record's 512 arrivals at one address.)
+constexpr uint32_t kUGroups = 16;
+constexpr uint32_t kUArrStride = 32 * (1 + kUGroups);
+
+typedef uint32_t enet_v4u __attribute__((ext_vector_type(4)));
+// 16-byte write-through store (sc1): the line leaves this XCD's L2 for memory (MI355X_MICROARCH.md,
+// inter-workgroup visibility).  asm stores are not in hipcc's vmcnt bookkeeping: the caller drains
+// with s_waitcnt vmcnt(0) before publishing; s_nop 1 keeps the next instruction off the data VGPRs.
+__device__ __forceinline__ void store_wt16(uint8_t* p, uint4 v) {
+    enet_v4u w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+}
+
+// Sum of the 320 threads' accumulators (the power wave contributes zero) into thread `who`'s l.
+// pw (nullable): the r^(2^k) table; data wave w's sum is then scaled by r^(1024 (3 - w)) first
+// (whole tiles: lane j's run ends 16 (255 - j) blocks before the tile's end, the in-wave part of
+// that scaling is the caller's)
+__device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [5][5] shared */, uint32_t who = 0,
+                                        const uint32_t* pw = nullptr) {
+#pragma unroll
+    for (int off = 1; off <= 8; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+    const uint32_t w = threadIdx.x >> 6;
+    if (pw && w < 3) pscale(l, (3u - w) << 10, pw, 12u);  // wave-uniform
+    if ((threadIdx.x & 63u) == 0) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) red[5 * w + i] = l[i];
+    }
+    __syncthreads();
+    if (threadIdx.x == who) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i] + red[20 + i];
+        pcarry(l);
+    }
+    __syncthreads();
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
+                                                                      uint32_t* __restrict__ arrivals) {
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kSegThreads * kRun];
+    __shared__ uint32_t red[25];
+    __shared__ uint32_t pw_s[kUPow * 5];  // r^(2^k), 26-bit limbs
+    __shared__ uint32_t t1_s[64 * 5];     // r^(16 i), i < 64: the in-wave part of a lane's scaling
+    __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
+    __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
+    __shared__ uint32_t last_flag;
+    const bool pwv = threadIdx.x >= kSegThreads;
+    const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
+    const uint32_t j = threadIdx.x;  // data lane (< 256 in the data waves)
+
+    const uint32_t rec = blockIdx.x / T, tr = blockIdx.x % T;
+    const uint64_t ioff = p.in_off[rec], iend = p.in_off[rec + 1];
+    // disordered offsets or an impossible length: handled as an empty record by the fallback
+    const uint64_t L = (iend >= ioff && iend - ioff < kSegMaxLen) ? iend - ioff : 0;
+    const bool as_hinted = iend >= ioff && L == Lh;
+    if (!as_hinted && tr != 0) return;  // the record's tile-0 workgroup runs it whole
+    const uint8_t* src = p.in + ioff;
+    uint8_t* dst = p.out + p.out_off[rec];
+    uint32_t kw[8], nw[3];
+    {
+        const uint32_t* kp = reinterpret_cast<const uint32_t*>(p.keys + (size_t)p.key_stride * rec);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kw[i] = kp[i];
+        const uint32_t* np = reinterpret_cast<const uint32_t*>(p.nonces + 12ull * rec);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) nw[i] = np[i];
+    }
+    ChachaRecord R;
+    chacha_record_init(R, kw, nw);
+    uint32_t aad_len = 0;
+    uint64_t aoff = 0;
+    if (p.aad) {
+        aoff = p.aad_off[rec];
+        aad_len = (uint32_t)(p.aad_off[rec + 1] - aoff);
+    }
+    const uint32_t na = (aad_len + 15) >> 4;
+    const uint32_t nct = (uint32_t)((L + 15) >> 4);
+    const uint32_t K = na + nct + 1;  // Poly1305 blocks
+    const uint32_t nb = (uint32_t)((L + 63) >> 6);
+    const uint32_t nt = as_hinted ? T : (L ? (uint32_t)((L + kTileBytes - 1) / kTileBytes) : 1u);
+    // combine geometry (main path): q right-aligned tiles per lane, q a power of two
+    const uint32_t nw_t = nt - 1;
+    uint32_t lq = 0;
+    while ((kSegThreads << lq) < nw_t) ++lq;
+    const uint32_t top = max(13u, min(12 + lq + 8, kUPow));  // table entries the combine reads: k < top
+
+    // ---- the power wave: the one-time key into LDS before barrier A; then (while the data waves
+    // run the tile) the table r^(2^k), k < top, and r^R before barrier B
+    if (pwv) {
+        uint32_t otk[16];
+#ifdef ENET_SEG_PROBE_NO_OTK
+        for (int i = 0; i < 16; ++i) otk[i] = R.k[i & 7];
+#else
+        chacha_block(R, 0u, otk);
+#endif
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) ok_s[i] = otk[i];
+        }
+    }
+    auto power_table = [&]() {  // the power wave, after barrier A
+#ifdef ENET_SEG_PROBE_NO_TABLE
+        return;
+#endif
+        uint32_t x[5];
+        pclamp(x, ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
+        auto put = [&](uint32_t k) {
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) pw_s[5 * k + i] = x[i];
+            }
+        };
+        for (uint32_t k = 0; k < 10; ++k) {
+            put(k);
+            pmul_by(x, x);
+        }
+        ENET_WAVE_LDS_SYNC();
+        // lane i: r^(16 i) from entries 4..9, beside the squarings k = 10..15 (independent chains)
+        uint32_t y[5] = {1, 0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t b = 0; b < 6; ++b) {
+            uint32_t m[5];
+            const bool on = (lane >> b) & 1u;
+#pragma unroll
+            for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (4 + b) + i] : (i == 0 ? 1u : 0u);
+            pmul_by(y, m);
+            put(10 + b);
+            pmul_by(x, x);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) t1_s[5 * lane + i] = y[i];
+        for (uint32_t k = 16; k < top; ++k) {
+            put(k);
+            pmul_by(x, x);
+        }
+        if (nw_t) {  // R = K - (na + 4096 nw) <= 4097
+            uint32_t y[5] = {1, 0, 0, 0, 0};
+            ENET_WAVE_LDS_SYNC();
+            pscale(y, K - (na + kTilePoly * nw_t), pw_s, 13u);
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < 5; ++i) rr_s[i] = y[i];
+            }
+        }
+    };
+
+    uint32_t hf[5] = {0, 0, 0, 0, 0};  // the record's Poly1305 sum (thread 0), normalised at K
+    PolyR32 PR{};
+    if (!as_hinted) {
+        // fallback: the whole record here, tile after tile, per lane (lane j: blocks [tb0 + 4j, +4))
+        __syncthreads();  // barrier A: r / s in LDS
+        PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
+        if (pwv) power_table();
+        uint32_t prev_end = 0;
+        for (uint32_t v = 0; v < nt; ++v) {
+            const uint32_t tb0 = v * kTileBlocks;
+            const uint32_t tb1 = min(tb0 + kTileBlocks, nb);
+            const uint32_t c0 = min(tb0 + kSegBPL * j, tb1), c1 = min(c0 + kSegBPL, tb1);
+            uint32_t h[5] = {0, 0, 0, 0, 0};
+            uint32_t l[5] = {0, 0, 0, 0, 0};
+            const bool last_tile = tb1 == nb;
+            const uint32_t tile_end = na + min(4u * tb1, nct) + (last_tile ? 1u : 0u);
+            if (!pwv) {
+                if (v == 0 && j == 0) {
+                    const uint8_t* ap = p.aad + aoff;
+                    for (uint32_t s2 = 0; s2 < na; ++s2) {
+                        const uint32_t cnt = min(16u, aad_len - 16u * s2);
+                        uint32_t w[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            uint32_t vv = 0;
+#pragma unroll
+                            for (int b2 = 0; b2 < 4; ++b2)
+                                if ((uint32_t)(4 * i + b2) < cnt) vv |= (uint32_t)ap[16 * s2 + 4 * i + b2] << (8 * b2);
+                            w[i] = vv;
+                        }
+                        poly32_block(h, PR, w[0], w[1], w[2], w[3], 1u);
+                    }
+                }
+                for (uint32_t c = c0; c < c1; ++c) {
+                    const uint64_t pos = 64ull * c;
+                    const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
+                    uint32_t w[16];
+                    load_block(src + pos, nbytes, w, pos + nbytes >= 16);
+                    uint32_t o[16];
+                    chacha_block(R, 1u + c, o);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[i] ^= w[i];
+                    store_block(dst + pos, nbytes, o);
+                    uint32_t* ct = (MODE == MODE_SEAL) ? o : w;
+                    if (MODE == MODE_SEAL && nbytes < 64) mask_tail(ct, nbytes);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (4 * c + u < nct)
+                            poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
+                }
+                const bool has_last = (c1 == nb && c1 > c0) || (nb == 0 && j == 0);
+                if (has_last) poly32_block(h, PR, aad_len, 0u, (uint32_t)L, (uint32_t)(L >> 32), 1u);
+                h32_to_limbs(h, l);
+            }
+            if (v == 0) __syncthreads();  // barrier B: the table in LDS
+            if (!pwv) {
+                const bool has_last = (c1 == nb && c1 > c0) || (nb == 0 && j == 0);
+                const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
+                if (c1 > c0 || (v == 0 && j == 0)) pscale(l, tile_end - lane_end, pw_s, 13u);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wg_sum5(l, red);
+            if (threadIdx.x == 0) {  // H = H r^(tile_end - prev_end) + P_v
+                pscale(hf, tile_end - prev_end, pw_s, 13u);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) hf[i] += l[i];
+                pcarry(hf);
+            }
+            prev_end = tile_end;
+        }
+    } else {
+        const uint32_t tt = tr;  // tile index inside the record
+        const uint32_t tb0 = tt * kTileBlocks;
+        const uint32_t tb1 = min(tb0 + kTileBlocks, nb);
+        const uint32_t c0 = min(tb0 + kSegBPL * j, tb1), c1 = min(c0 + kSegBPL, tb1);
+        const bool whole = (uint64_t)(tb0 + kTileBlocks) * 64ull <= L;  // uniform over the workgroup
+        const bool first_iter = true;
+        uint32_t h[5] = {0, 0, 0, 0, 0};
+        auto barrier_a = [&]() {  // r / s in LDS
+            __syncthreads();
+            PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
+        };
+        auto absorb_aad = [&]() {
+            if (tt == 0 && j == 0 && !pwv) {
+                const uint8_t* ap = p.aad + aoff;
+                for (uint32_t s = 0; s < na; ++s) {
+                    const uint32_t cnt = min(16u, aad_len - 16u * s);
+                    uint32_t w[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint32_t vv = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            if ((uint32_t)(4 * i + b) < cnt) vv |= (uint32_t)ap[16 * s + 4 * i + b] << (8 * b);
+                        w[i] = vv;
+                    }
+                    poly32_block(h, PR, w[0], w[1], w[2], w[3], 1u);
+                }
+            }
+        };
+        if (whole) {
+            const uint32_t kk = lane & 7u;
+            const uint32_t msw = slab_sw(lane);
+            uint8_t* wslab = slab + wbase * kRun;
+            uint8_t* myrun = slab + threadIdx.x * kRun;
+            const uint8_t* ib = src + 64ull * tb0;
+            uint8_t* ob = dst + 64ull * tb0;
+            const bool nt_ok = ((reinterpret_cast<uintptr_t>(ob)) & 63u) == 0;
+            uint32_t offs[8];
+            uint32_t pf[32];
+            if (!pwv) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint32_t o = 8u * i + (lane >> 3);
+                    offs[i] = 64u * kSegBPL * (wbase + o) + 16u * (kk ^ slab_sw(o));
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(ib + offs[i]);
+                    pf[4 * i] = q.x; pf[4 * i + 1] = q.y; pf[4 * i + 2] = q.z; pf[4 * i + 3] = q.w;
+                }
+            }
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                uint32_t w2[32], ka[16], kb[16];
+                if (!pwv) {
+                    ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        *reinterpret_cast<uint4*>(wslab + 1024u * i + 16u * lane) =
+                            make_uint4(pf[4 * i], pf[4 * i + 1], pf[4 * i + 2], pf[4 * i + 3]);
+                    ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint4 q = *reinterpret_cast<const uint4*>(myrun + 16u * (k ^ msw));
+                        w2[4 * k] = q.x; w2[4 * k + 1] = q.y; w2[4 * k + 2] = q.z; w2[4 * k + 3] = q.w;
+                    }
+                    if (st == 0) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const uint4 q = *reinterpret_cast<const uint4*>(ib + offs[i] + kRun);
+                            pf[4 * i] = q.x; pf[4 * i + 1] = q.y; pf[4 * i + 2] = q.z; pf[4 * i + 3] = q.w;
+                        }
+                        asm volatile("" : "+v"(R.k[0])::"memory");
+                    }
+                    const uint32_t cb = 1u + c0 + 2u * st;  // RFC 8439 data counter from 1
+                    chacha_block2(R, cb, cb + 1u, ka, kb);
+                }
+                if (st == 0 && first_iter) {
+                    barrier_a();
+                    absorb_aad();
+                } else if (st == 0) {
+                    PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
+                    absorb_aad();
+                }
+                if (!pwv) {
+#ifndef ENET_SEG_PROBE_NO_POLY
+                    if (MODE == MODE_OPEN) {
+                        poly_block64(h, PR, w2);
+                        poly_block64(h, PR, w2 + 16);
+                    }
+#endif
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
+#ifndef ENET_SEG_PROBE_NO_POLY
+                    if (MODE == MODE_SEAL) {
+                        poly_block64(h, PR, w2);
+                        poly_block64(h, PR, w2 + 16);
+                    }
+#else
+                    h[0] ^= w2[0];
+#endif
+                    ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        *reinterpret_cast<uint4*>(myrun + 16u * (k ^ msw)) =
+                            make_uint4(w2[4 * k], w2[4 * k + 1], w2[4 * k + 2], w2[4 * k + 3]);
+                    ENET_WAVE_LDS_SYNC();
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint4 q = *reinterpret_cast<const uint4*>(wslab + 1024u * i + 16u * lane);
+                        if (MODE == MODE_OPEN) store_wt16(ob + offs[i] + kRun * st, q);
+                        else store_stream(ob + offs[i] + kRun * st, q, nt_ok);
+                    }
+                }
+            }
+        } else {
+            if (first_iter) barrier_a();
+            else PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
+            absorb_aad();
+            if (!pwv) {
+                for (uint32_t c = c0; c < c1; ++c) {
+                    const uint64_t pos = 64ull * c;
+                    const uint32_t nbytes = (uint32_t)min<uint64_t>(64, L - pos);
+                    uint32_t w[16];
+                    load_block(src + pos, nbytes, w, pos + nbytes >= 16);
+                    uint32_t o[16];
+                    chacha_block(R, 1u + c, o);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) o[i] ^= w[i];
+                    if (MODE == MODE_OPEN && nbytes == 64) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            store_wt16(dst + pos + 16 * q, make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
+                    } else if (MODE == MODE_OPEN) {
+                        // the record's last partial block, write-through byte by byte (a failed
+                        // record is zeroed by another workgroup, whose stores must land last)
+                        for (uint32_t b = 0; b < nbytes; ++b)
+                            __hip_atomic_store(dst + pos + b, (uint8_t)(o[b >> 2] >> (8 * (b & 3))), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        store_block(dst + pos, nbytes, o);
+                    }
+                    uint32_t* ct = (MODE == MODE_SEAL) ? o : w;
+                    if (MODE == MODE_SEAL && nbytes < 64) mask_tail(ct, nbytes);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (4 * c + u < nct)
+                            poly32_block(h, PR, ct[4 * u], ct[4 * u + 1], ct[4 * u + 2], ct[4 * u + 3], 1u);
+                }
+            }
+        }
+
+        // this tile's partial, normalised at the tile's end
+        uint32_t l[5] = {0, 0, 0, 0, 0};
+        const bool last_tile = tb1 == nb;
+        const uint32_t tile_end = na + min(4u * tb1, nct) + (last_tile ? 1u : 0u);
+        const bool has_last = (c1 == nb && c1 > c0) || (nb == 0 && j == 0);
+        if (!pwv) {
+            if (has_last) poly32_block(h, PR, aad_len, 0u, (uint32_t)L, (uint32_t)(L >> 32), 1u);
+            h32_to_limbs(h, l);
+        }
+#ifdef ENET_SEG_PROBE_NO_PUBLISH
+        if (h[0] == 0x12345u) p.ok[rec] = 7;  // keep the Horner live
+        return;
+#endif
+        // the power wave skipped the tile's body: it builds the table here, where no tile data
+        // is live (inside the body its registers would count against every wave)
+        if (pwv) power_table();
+#ifndef ENET_SEG_PROBE_NO_SYNC
+        __syncthreads();  // barrier B: the table in LDS
+#endif
+#ifndef ENET_SEG_PROBE_NO_SCALE
+        if (!pwv) {
+            const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
+            const uint32_t e = tile_end - lane_end;
+            if (whole) {
+                // e = 16 (255 - j) (+1 in the record's last tile for lanes before the length
+                // block): r^(16 (63 - lane)) here, r^(1024 (3 - wave)) on the wave's sum
+                uint32_t m[5];
+#pragma unroll
+                for (int i = 0; i < 5; ++i) m[i] = t1_s[5 * (63u - lane) + i];
+                pmul_by(l, m);
+                if (e != 16u * (255u - j)) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) m[i] = pw_s[i];
+                    pmul_by(l, m);
+                }
+            } else if (c1 > c0 || (tt == 0 && j == 0)) {
+                pscale(l, e, pw_s, 13u);
+            }
+        }
+#endif
+        // open: every wave drains its write-through plaintext before the arrival (the last arriver
+        // may zero the record); seal: the ciphertext stores stay in flight -- the power wave, which
+        // stored nothing, publishes, so its vmcnt(0) waits for the partial alone
+        if (MODE == MODE_OPEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wg_sum5(l, red, kSegThreads, whole ? pw_s : nullptr);
+        // main path: publish, take a ticket; the last tile of the record to arrive finishes it
+        uint32_t* part = p.partials + 8ull * blockIdx.x;
+        uint32_t* ctr = arrivals + (size_t)kUArrStride * rec;  // [0] top, [32 (1 + g)] group g
+        if (threadIdx.x == kSegThreads) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) __hip_atomic_store(part + i, l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t ng = min(T, kUGroups), g = tt % ng, members = (T - g + ng - 1) / ng;
+            uint32_t* gc = ctr + 32 * (1 + g);
+            const uint32_t prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t lf = 0;
+            if (prev + 1 == members) {  // the group is complete: reset it, arrive at the top
+                __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t top_prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lf = top_prev + 1 == ng ? 1u : 0u;
+            }
+            last_flag = lf;
+        }
+        __syncthreads();
+#ifdef ENET_SEG_PROBE_NO_TAIL
+        if (threadIdx.x == 0 && last_flag) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+#endif
+        if (!last_flag) return;  // uniform over the workgroup
+        const uint32_t* parts = p.partials + 8ull * ((size_t)rec * T);
+        uint32_t vl[5] = {0, 0, 0, 0, 0};  // the last tile's partial, normalised at K: loaded first
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) vl[i] = __hip_atomic_load(parts + 8ull * (T - 1) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        auto pw_at = [&](uint32_t k, uint32_t out[5]) {  // r^(2^k) from this workgroup's table
+#pragma unroll
+            for (int i = 0; i < 5; ++i) out[i] = pw_s[5 * k + i];
+        };
+        uint32_t acc[5] = {0, 0, 0, 0, 0};
+        if (nw_t) {
+            if (!pwv) {
+                const uint32_t q = 1u << lq;
+                const int64_t hi = (int64_t)nw_t - (int64_t)q * (kSegThreads - 1 - j);
+                const int64_t lo = max<int64_t>(0, hi - (int64_t)q);
+                uint32_t m[5];
+                pw_at(12, m);
+                const Pmul M4 = pmul_make(m);
+                uint32_t nx[5] = {0, 0, 0, 0, 0};
+                if (lo < hi) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) nx[i] = __hip_atomic_load(parts + 8 * lo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                for (int64_t t = lo; t < hi; ++t) {
+                    uint32_t cur[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) cur[i] = nx[i];
+                    if (t + 1 < hi) {  // the next partial's load flies under this step
+#pragma unroll
+                        for (int i = 0; i < 5; ++i)
+                            nx[i] = __hip_atomic_load(parts + 8 * (t + 1) + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (t > lo) pmul(acc, M4);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) acc[i] += cur[i];
+                    pcarry(acc);
+                }
+#pragma unroll
+                for (uint32_t d = 1, lev = 0; d < 64; d <<= 1, ++lev) {
+                    uint32_t o[5], x[5], mm[5];
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) o[i] = __shfl_xor(acc[i], (int)d);
+                    const bool left = (lane & d) == 0u;  // the earlier tiles
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) {
+                        x[i] = left ? acc[i] : o[i];
+                        o[i] = left ? o[i] : acc[i];
+                    }
+                    pw_at(12 + lq + lev, mm);
+                    pmul_by(x, mm);
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) acc[i] = x[i] + o[i];
+                    pcarry(acc);
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) red[5 * (threadIdx.x >> 6) + i] = acc[i];
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t A[5], B[5], m6[5], m7[5], rr[5];
+                pw_at(12 + lq + 6, m6);
+                pw_at(12 + lq + 7, m7);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) { A[i] = red[i]; B[i] = red[10 + i]; }
+                pmul_by(A, m6);
+                pmul_by(B, m6);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) { A[i] += red[5 + i]; B[i] += red[15 + i]; }
+                pcarry(A);
+                pcarry(B);
+                pmul_by(A, m7);
+#pragma unroll
+                for (int i = 0; i < 5; ++i) { acc[i] = A[i] + B[i]; rr[i] = rr_s[i]; }
+                pcarry(acc);
+                pmul_by(acc, rr);
+            }
+        }
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) hf[i] = acc[i] + vl[i];
+            pcarry(hf);
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+        }
+    }
+    // tag / verdict; a failed open's plaintext is zeroed here (every tile's stores were
+    // write-through and drained before its arrival; the fallback's are this workgroup's own)
+    if (threadIdx.x == 0) {
+        uint32_t tag[4];
+        pfinish(hf, ok_s + 4, tag);
+        if (MODE == MODE_SEAL) {
+            uint32_t* tp = reinterpret_cast<uint32_t*>(p.tag_out + 16ull * rec);
+            tp[0] = tag[0]; tp[1] = tag[1]; tp[2] = tag[2]; tp[3] = tag[3];
+        } else {
+            const uint32_t* tp = reinterpret_cast<const uint32_t*>(p.tag_in + 16ull * rec);
+            const uint32_t diff = (tag[0] ^ tp[0]) | (tag[1] ^ tp[1]) | (tag[2] ^ tp[2]) | (tag[3] ^ tp[3]);
+            p.ok[rec] = diff == 0 ? 1 : 0;
+            last_flag = diff == 0 ? 0u : 1u;  // reused: 1 = zero the record
+        }
+    }
+#if defined(ENET_SEG_PROBE_NO_POLY) || defined(ENET_SEG_PROBE_NO_TABLE)
+    if (MODE == MODE_OPEN) return;  // timing probes: wrong tags, nothing to zero
+#endif
+    if (MODE == MODE_OPEN) {
+        __syncthreads();
+        if (last_flag) {
+            for (uint64_t b = 16ull * threadIdx.x; b < L; b += 16ull * kUThreads) {
+                const uint32_t nbytes = (uint32_t)min<uint64_t>(16, L - b);
+                if (nbytes == 16 && ((reinterpret_cast<uintptr_t>(dst + b)) & 15u) == 0)
+                    *reinterpret_cast<uint4*>(dst + b) = make_uint4(0u, 0u, 0u, 0u);
+                else
+                    for (uint32_t t = 0; t < nbytes; ++t) dst[b + t] = 0;
+            }
+        }
+    }
+}
+
 // dst[width * list[k] ..] = src[width * k ..] for k < m (results computed on the host for a subset
 // of the batch, e.g. the host-hashed digests of long chunks, capi.cpp)
 __global__ void scatter_kernel(const uint8_t* __restrict__ src, const uint32_t* __restrict__ list, uint32_t m,
@@ -561,6 +1154,27 @@ hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, 
 }
 
 // ---------------------------------------------------------------------------------- host side
+uint32_t seg_uniform_arrival_words() { return kUArrStride; }
+
+hipError_t launch_seg_uniform_aead(const SegParams& p, uint64_t L, uint32_t* arrivals, hipStream_t s) {
+    const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
+    const uint64_t blocks = (uint64_t)p.n * T;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7FFFFFFFull || T > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    switch (p.mode) {
+        case MODE_SEAL:
+            hipLaunchKernelGGL(seg_uniform_aead_kernel<MODE_SEAL>, dim3((uint32_t)blocks), dim3(kUThreads), 0, s, p, L,
+                               (uint32_t)T, arrivals);
+            break;
+        case MODE_OPEN:
+            hipLaunchKernelGGL(seg_uniform_aead_kernel<MODE_OPEN>, dim3((uint32_t)blocks), dim3(kUThreads), 0, s, p, L,
+                               (uint32_t)T, arrivals);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_seg_uniform_xor(const SegParams& p, uint64_t L, hipStream_t s) {
     const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
     const uint64_t blocks = (uint64_t)p.n * T;

@@ -234,3 +234,77 @@ def test_seg_uniform_xor_one_launch_and_lying_hints(enet, lens):
         for i in range(n):
             want = oracle.chacha20_xor(keys[i], nonces[i], items[i], int(ctr[i]))
             assert oh[offs[i]:offs[i + 1]] == want, f"record {i} (len {lens[i]}, in place {inplace})"
+
+
+@pytest.mark.parametrize("with_aad", [False, True])
+@pytest.mark.parametrize("lens", [[300 << 10] * 5, [300 << 10, 100, (600 << 10) + 7, 0, 300 << 10, 65536 + 1, 4095]])
+def test_seg_uniform_aead_one_launch_lying_hints_tamper(enet, lens, with_aad):
+    """RFC 8439 seal / open over a batch the hints call uniform (n x 300 KiB): one launch -- each
+    record's last tile to arrive combines the partials and, on open, zeroes a failed record itself
+    (write-through plaintext).  The second shape lies: records of 100 B, 600 KiB + 7, 0, 64 KiB + 1
+    and 4 095 B under the 300 KiB hint are run whole by their tile-0 workgroups.  Bit-exact vs the
+    oracle (tags pinned by RFC 8439 / OpenSSL through the oracle's golden checks), every record
+    opens; then a flipped tag on an as-hinted record, a flipped ciphertext byte in another and in
+    a fallback record: those three fail and are zeroed, the rest open.  Runs twice: the per-stream
+    arrival counters must be back at zero for the second launch."""
+    import torch
+    n = len(lens)
+    b, items, keys, nonces = make(enet, lens, 9600 + len(lens) + (7 if with_aad else 0))
+    hint = dict(total_bytes_hint=n * (300 << 10), max_len_hint=300 << 10)
+    aads = [splitmix_bytes(9900 + i, (i * 37) % 90) for i in range(n)] if with_aad else None
+    aad = aad_off = None
+    if with_aad:
+        ao = [0]
+        for a_ in aads:
+            ao.append(ao[-1] + len(a_))
+        aad = torch.frombuffer(bytearray(b"".join(aads) or b"\0"), dtype=torch.uint8).cuda()
+        aad_off = torch.tensor(ao, dtype=torch.int64, device="cuda")
+    offs = b.offsets.cpu().tolist()
+    sb = enet.Batch(b.arena, b.offsets, b.keys, b.nonces, **hint)
+    for rep in range(2):
+        ct = torch.zeros_like(b.arena)
+        tags = torch.zeros(16 * n, dtype=torch.uint8, device="cuda")
+        before = enet.seg_batches()
+        enet.aead_seal(sb, ct, tags, aad=aad, aad_offsets=aad_off)
+        torch.cuda.synchronize()
+        assert enet.seg_batches() == before + 1
+        cth, th = host(ct), host(tags)
+        for i in range(n):
+            c, t = oracle.aead_seal(keys[i], nonces[i], items[i], aads[i] if with_aad else b"")
+            assert cth[offs[i]:offs[i + 1]] == c, f"ciphertext {i} (len {lens[i]}, rep {rep})"
+            assert th[16 * i:16 * i + 16] == t, f"tag {i} (len {lens[i]}, rep {rep})"
+        ob = enet.Batch(ct, b.offsets, b.keys, b.nonces, **hint)
+        back = torch.full_like(ct, 0xAA)
+        ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        enet.aead_open(ob, back, tags, ok, aad=aad, aad_offsets=aad_off)
+        torch.cuda.synchronize()
+        assert ok.cpu().tolist() == [1] * n, rep
+        bh = host(back)
+        for i in range(n):
+            assert bh[offs[i]:offs[i + 1]] == items[i], f"plaintext {i} (rep {rep})"
+    # tamper
+    hinted = [i for i in range(n) if lens[i] == 300 << 10]
+    fallback = [i for i in range(n) if lens[i] != 300 << 10 and lens[i] > 0]
+    bad_tags = tags.clone()
+    bad_tags[16 * hinted[0] + 3] ^= 0x40
+    ct2 = ct.clone()
+    victims = {hinted[0]}
+    if len(hinted) > 1:
+        ct2[offs[hinted[1]] + 150_000] ^= 0x01
+        victims.add(hinted[1])
+    if fallback:
+        f = fallback[-1]
+        ct2[offs[f] + lens[f] // 2] ^= 0x02
+        victims.add(f)
+    ob2 = enet.Batch(ct2, b.offsets, b.keys, b.nonces, **hint)
+    back = torch.full_like(ct, 0xAA)
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    enet.aead_open(ob2, back, bad_tags, ok, aad=aad, aad_offsets=aad_off)
+    torch.cuda.synchronize()
+    okh, bh = ok.cpu().tolist(), host(back)
+    for i in range(n):
+        if i in victims:
+            assert okh[i] == 0, f"tampered record {i} verified"
+            assert bh[offs[i]:offs[i + 1]] == bytes(lens[i]), f"tampered record {i} released plaintext"
+        else:
+            assert okh[i] == 1 and bh[offs[i]:offs[i + 1]] == items[i], f"record {i}"

@@ -46,7 +46,7 @@ STALL_PASSES = [
 
 def kernel_key(name: str):
     if not any(k in name for k in ("records_kernel", "sha_kernel", "stream_kernel", "duplex_kernel",
-                                   "duplex_split_kernel")):
+                                   "duplex_split_kernel", "seg_uniform", "seg_kernel", "seg_plan")):
         return None
     return name.split("(")[0].replace("void ", "")
 
