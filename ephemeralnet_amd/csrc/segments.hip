@@ -565,6 +565,14 @@ __global__ __launch_bounds__(kSegThreads) void seg_uniform_xor_kernel(SegParams 
 //   * a record whose real length differs from the hint is run whole by its tile-0 workgroup, tile
 //     after tile, its partials combined in that workgroup (a wrong hint costs speed, never bytes).
 constexpr uint32_t kUThreads = kSegThreads + 64;   // four data waves + the power wave
+#ifdef ENET_SEG_PROBE_TRACE
+// timing probe: per-workgroup wall-clock stamps (100 MHz) at the phase boundaries, read back by
+// tools/seg_trace.py through enet_probe_trace_read (hand-built libraries only)
+__device__ uint64_t g_seg_trace[8192 * 8];
+#define SEG_STAMP(k) (g_seg_trace[8ull * blockIdx.x + (k)] = wall_clock64())
+#else
+#define SEG_STAMP(k) ((void)0)
+#endif
 constexpr uint32_t kUPow = 44;                      // LDS table entries r^(2^k), k < 44
 // Arrival counters per record: a top counter and kUGroups group counters, each on its own 128-byte
 // line.  Tile t arrives at group t mod kUGroups; a group's last arriver arrives at the top counter.
@@ -581,12 +589,21 @@ __device__ __forceinline__ void store_wt16(uint8_t* p, uint4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
 }
 
+// Workgroup barrier for LDS hand-offs only: this wave's LDS operations retire, then s_barrier.
+// __syncthreads() also drains the wave's outstanding global stores (vmcnt(0)): after a tile's
+// stores that held every wave for their round trip at each barrier.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // Sum of the 320 threads' accumulators (the power wave contributes zero) into thread `who`'s l.
 // pw (nullable): the r^(2^k) table; data wave w's sum is then scaled by r^(1024 (3 - w)) first
 // (whole tiles: lane j's run ends 16 (255 - j) blocks before the tile's end, the in-wave part of
 // that scaling is the caller's)
 __device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [5][5] shared */, uint32_t who = 0,
-                                        const uint32_t* pw = nullptr) {
+                                        const uint32_t* pw = nullptr, uint32_t nwaves = 5) {
 #pragma unroll
     for (int off = 1; off <= 8; off <<= 1) {
 #pragma unroll
@@ -605,17 +622,22 @@ __device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [5][5] s
 #pragma unroll
         for (int i = 0; i < 5; ++i) red[5 * w + i] = l[i];
     }
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == who) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) l[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i] + red[20 + i];
+        for (int i = 0; i < 5; ++i) l[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i] + (nwaves > 4 ? red[20 + i] : 0u);
         pcarry(l);
     }
-    __syncthreads();
+    lds_barrier();
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
+#ifdef ENET_SEG_PROBE_LB4
+#define ENET_UAEAD_BOUNDS __launch_bounds__(kUThreads, 4)
+#else
+#define ENET_UAEAD_BOUNDS __launch_bounds__(kUThreads)
+#endif
+__global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
                                                                       uint32_t* __restrict__ arrivals) {
     __shared__ __attribute__((aligned(16))) uint8_t slab[kSegThreads * kRun];
     __shared__ uint32_t red[25];
@@ -624,11 +646,18 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
     __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
     __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
     __shared__ uint32_t last_flag;
+    __shared__ uint32_t tab_s;  // 1: the high part of the table is in LDS (main path)
     const bool pwv = threadIdx.x >= kSegThreads;
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
     const uint32_t j = threadIdx.x;  // data lane (< 256 in the data waves)
 
     const uint32_t rec = blockIdx.x / T, tr = blockIdx.x % T;
+    if (threadIdx.x == 0) SEG_STAMP(0);
+#ifdef ENET_SEG_PROBE_TRACE
+    if (threadIdx.x == 0)  // where the workgroup runs: HW_ID (cu, sh, se) and XCC_ID
+        g_seg_trace[8ull * blockIdx.x + 7] = ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11)) << 32) |
+                                             (uint32_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+#endif
     const uint64_t ioff = p.in_off[rec], iend = p.in_off[rec + 1];
     // disordered offsets or an impossible length: handled as an empty record by the fallback
     const uint64_t L = (iend >= ioff && iend - ioff < kSegMaxLen) ? iend - ioff : 0;
@@ -676,42 +705,49 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) ok_s[i] = otk[i];
+            tab_s = 0;
         }
     }
-    auto power_table = [&]() {  // the power wave, after barrier A
+    // The power wave's table, in two parts.  Low (before barrier B; what the tile's own scaling
+    // reads): r^(2^k), k <= 12, and in lane i r^(16 i) -- the product of r^(2^(4+b)) over the bits b
+    // of i, taken from the running square as it passes (a second chain beside the squarings).
+    // High (main path: after barrier B, while the data waves publish; read only by the record's
+    // last arriver, which waits for tab_s): r^(2^k), 13 <= k < top, and r^R.
+    uint32_t px[5];  // the power wave's running square
+    auto put = [&](uint32_t k) {
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < 5; ++i) pw_s[5 * k + i] = px[i];
+        }
+    };
+    auto power_low = [&]() {
 #ifdef ENET_SEG_PROBE_NO_TABLE
         return;
 #endif
-        uint32_t x[5];
-        pclamp(x, ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
-        auto put = [&](uint32_t k) {
-            if (lane == 0) {
-#pragma unroll
-                for (int i = 0; i < 5; ++i) pw_s[5 * k + i] = x[i];
-            }
-        };
-        for (uint32_t k = 0; k < 10; ++k) {
-            put(k);
-            pmul_by(x, x);
-        }
-        ENET_WAVE_LDS_SYNC();
-        // lane i: r^(16 i) from entries 4..9, beside the squarings k = 10..15 (independent chains)
+        pclamp(px, ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
         uint32_t y[5] = {1, 0, 0, 0, 0};
 #pragma unroll
-        for (uint32_t b = 0; b < 6; ++b) {
-            uint32_t m[5];
-            const bool on = (lane >> b) & 1u;
+        for (uint32_t k = 0; k < 13; ++k) {
+            put(k);
+            if (k >= 4 && k < 10) {
+                uint32_t m[5];
+                const bool on = (lane >> (k - 4)) & 1u;
 #pragma unroll
-            for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (4 + b) + i] : (i == 0 ? 1u : 0u);
-            pmul_by(y, m);
-            put(10 + b);
-            pmul_by(x, x);
+                for (int i = 0; i < 5; ++i) m[i] = on ? px[i] : (i == 0 ? 1u : 0u);
+                pmul_by(y, m);
+            }
+            pmul_by(px, px);
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) t1_s[5 * lane + i] = y[i];
-        for (uint32_t k = 16; k < top; ++k) {
+    };
+    auto power_high = [&]() {
+#ifdef ENET_SEG_PROBE_NO_TABLE
+        return;
+#endif
+        for (uint32_t k = 13; k < top; ++k) {
             put(k);
-            pmul_by(x, x);
+            pmul_by(px, px);
         }
         if (nw_t) {  // R = K - (na + 4096 nw) <= 4097
             uint32_t y[5] = {1, 0, 0, 0, 0};
@@ -730,7 +766,10 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
         // fallback: the whole record here, tile after tile, per lane (lane j: blocks [tb0 + 4j, +4))
         __syncthreads();  // barrier A: r / s in LDS
         PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
-        if (pwv) power_table();
+        if (pwv) {
+            power_low();
+            power_high();
+        }
         uint32_t prev_end = 0;
         for (uint32_t v = 0; v < nt; ++v) {
             const uint32_t tb0 = v * kTileBlocks;
@@ -803,7 +842,8 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
         const bool first_iter = true;
         uint32_t h[5] = {0, 0, 0, 0, 0};
         auto barrier_a = [&]() {  // r / s in LDS
-            __syncthreads();
+            lds_barrier();
+            if (threadIdx.x == 0) SEG_STAMP(1);
             PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
         };
         auto absorb_aad = [&]() {
@@ -962,10 +1002,20 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
 #endif
         // the power wave skipped the tile's body: it builds the table here, where no tile data
         // is live (inside the body its registers would count against every wave)
-        if (pwv) power_table();
+        if (threadIdx.x == 0) SEG_STAMP(2);
+        if (pwv) power_low();
+        if (threadIdx.x == kSegThreads) SEG_STAMP(3);
 #ifndef ENET_SEG_PROBE_NO_SYNC
-        __syncthreads();  // barrier B: the table in LDS
+        lds_barrier();  // barrier B: the table's low part in LDS
 #endif
+        if (threadIdx.x == 0) SEG_STAMP(4);
+        if (pwv) {
+            // the high part, then the power wave leaves: the barriers below wait on the data waves
+            // alone (s_barrier counts the workgroup's surviving waves)
+            power_high();
+            __hip_atomic_store(&tab_s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
 #ifndef ENET_SEG_PROBE_NO_SCALE
         if (!pwv) {
             const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
@@ -988,14 +1038,13 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
         }
 #endif
         // open: every wave drains its write-through plaintext before the arrival (the last arriver
-        // may zero the record); seal: the ciphertext stores stay in flight -- the power wave, which
-        // stored nothing, publishes, so its vmcnt(0) waits for the partial alone
+        // may zero the record)
         if (MODE == MODE_OPEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wg_sum5(l, red, kSegThreads, whole ? pw_s : nullptr);
+        wg_sum5(l, red, 0, whole ? pw_s : nullptr, 4);
         // main path: publish, take a ticket; the last tile of the record to arrive finishes it
         uint32_t* part = p.partials + 8ull * blockIdx.x;
         uint32_t* ctr = arrivals + (size_t)kUArrStride * rec;  // [0] top, [32 (1 + g)] group g
-        if (threadIdx.x == kSegThreads) {
+        if (threadIdx.x == 0) {
 #pragma unroll
             for (int i = 0; i < 5; ++i) __hip_atomic_store(part + i, l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1009,8 +1058,9 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
                 lf = top_prev + 1 == ng ? 1u : 0u;
             }
             last_flag = lf;
+            SEG_STAMP(5);
         }
-        __syncthreads();
+        lds_barrier();
 #ifdef ENET_SEG_PROBE_NO_TAIL
         if (threadIdx.x == 0 && last_flag) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -1054,6 +1104,9 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
                     for (int i = 0; i < 5; ++i) acc[i] += cur[i];
                     pcarry(acc);
                 }
+                // the high part of the table (the power wave's, after barrier B)
+                while (__hip_atomic_load(&tab_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                    __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                 for (uint32_t d = 1, lev = 0; d < 64; d <<= 1, ++lev) {
                     uint32_t o[5], x[5], mm[5];
@@ -1105,6 +1158,7 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
     }
     // tag / verdict; a failed open's plaintext is zeroed here (every tile's stores were
     // write-through and drained before its arrival; the fallback's are this workgroup's own)
+    if (threadIdx.x == 0) SEG_STAMP(6);
     if (threadIdx.x == 0) {
         uint32_t tag[4];
         pfinish(hf, ok_s + 4, tag);
@@ -1123,8 +1177,9 @@ __global__ __launch_bounds__(kUThreads) void seg_uniform_aead_kernel(SegParams p
 #endif
     if (MODE == MODE_OPEN) {
         __syncthreads();
-        if (last_flag) {
-            for (uint64_t b = 16ull * threadIdx.x; b < L; b += 16ull * kUThreads) {
+        const uint32_t zt = as_hinted ? kSegThreads : kUThreads;  // the main path's power wave has left
+        if (last_flag && threadIdx.x < zt) {
+            for (uint64_t b = 16ull * threadIdx.x; b < L; b += 16ull * zt) {
                 const uint32_t nbytes = (uint32_t)min<uint64_t>(16, L - b);
                 if (nbytes == 16 && ((reinterpret_cast<uintptr_t>(dst + b)) & 15u) == 0)
                     *reinterpret_cast<uint4*>(dst + b) = make_uint4(0u, 0u, 0u, 0u);
@@ -1155,6 +1210,12 @@ hipError_t launch_scatter(const uint8_t* src, const uint32_t* list, uint32_t m, 
 
 // ---------------------------------------------------------------------------------- host side
 uint32_t seg_uniform_arrival_words() { return kUArrStride; }
+
+#ifdef ENET_SEG_PROBE_TRACE
+extern "C" __attribute__((visibility("default"))) int enet_probe_trace_read(uint64_t* out, size_t n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_trace), 8 * std::min<size_t>(n, 8192 * 8)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_seg_uniform_aead(const SegParams& p, uint64_t L, uint32_t* arrivals, hipStream_t s) {
     const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
