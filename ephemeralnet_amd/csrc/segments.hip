@@ -67,6 +67,25 @@ __device__ __forceinline__ void pscale(uint32_t l[5], uint32_t e, const uint32_t
 // l <- l * m (26-bit limbs)
 __device__ __forceinline__ void pmul_by(uint32_t l[5], const uint32_t m[5]) { pmul(l, pmul_make(m)); }
 
+// h <- h^2 (mod 2^130-5): 15 products instead of pmul's 25; same bounds and reduction as pmul
+__device__ __forceinline__ void psquare(uint32_t h[5]) {
+    const uint64_t h0 = h[0], h1 = h[1], h2 = h[2], h3 = h[3], h4 = h[4];
+    const uint64_t t0 = 2 * h0, t1 = 2 * h1, f3 = 5 * h3, f4 = 5 * h4, g4 = 10 * h4;
+    uint64_t d0 = h0 * h0 + h1 * g4 + h2 * (2 * f3);
+    uint64_t d1 = t0 * h1 + h2 * g4 + h3 * f3;
+    uint64_t d2 = t0 * h2 + h1 * h1 + h3 * g4;
+    uint64_t d3 = t0 * h3 + t1 * h2 + h4 * f4;
+    uint64_t d4 = t0 * h4 + t1 * h3 + h2 * h2;
+    uint32_t c;
+    c = (uint32_t)(d0 >> 26); h[0] = (uint32_t)d0 & M26; d1 += c;
+    c = (uint32_t)(d1 >> 26); h[1] = (uint32_t)d1 & M26; d2 += c;
+    c = (uint32_t)(d2 >> 26); h[2] = (uint32_t)d2 & M26; d3 += c;
+    c = (uint32_t)(d3 >> 26); h[3] = (uint32_t)d3 & M26; d4 += c;
+    c = (uint32_t)(d4 >> 26); h[4] = (uint32_t)d4 & M26;
+    h[0] += c * 5u;
+    c = h[0] >> 26; h[0] &= M26; h[1] += c;
+}
+
 // Sum of the workgroup's 256 accumulators (limbs < 2^27) into thread 0's l (limbs < 2^27)
 __device__ __forceinline__ void wg_sum(uint32_t l[5], uint32_t* red /* [4][5] shared */) {
 #pragma unroll
@@ -564,7 +583,12 @@ __global__ __launch_bounds__(kSegThreads) void seg_uniform_xor_kernel(SegParams 
 //     by each record's last arriver;
 //   * a record whose real length differs from the hint is run whole by its tile-0 workgroup, tile
 //     after tile, its partials combined in that workgroup (a wrong hint costs speed, never bytes).
-constexpr uint32_t kUThreads = kSegThreads + 64;   // four data waves + the power wave
+// Two tiles per workgroup (eight data waves) + the power wave: nine waves of 152 VGPRs fit a CU
+// (three per SIMD), so a 32 MiB record's 512 tiles are all resident at once.  (One tile per
+// five-wave workgroup ran in two rounds: a second such workgroup did not fit beside the first.)
+constexpr uint32_t kUTiles = 2;
+constexpr uint32_t kUData = kSegThreads * kUTiles;  // data threads
+constexpr uint32_t kUThreads = kUData + 64;         // + the power wave
 #ifdef ENET_SEG_PROBE_TRACE
 // timing probe: per-workgroup wall-clock stamps (100 MHz) at the phase boundaries, read back by
 // tools/seg_trace.py through enet_probe_trace_read (hand-built libraries only)
@@ -598,12 +622,8 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// Sum of the 320 threads' accumulators (the power wave contributes zero) into thread `who`'s l.
-// pw (nullable): the r^(2^k) table; data wave w's sum is then scaled by r^(1024 (3 - w)) first
-// (whole tiles: lane j's run ends 16 (255 - j) blocks before the tile's end, the in-wave part of
-// that scaling is the caller's)
-__device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [5][5] shared */, uint32_t who = 0,
-                                        const uint32_t* pw = nullptr, uint32_t nwaves = 5) {
+// Sum of the first `nwaves` waves' accumulators into thread 0's l (the others contribute zero).
+__device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [waves][5] shared */, uint32_t nwaves) {
 #pragma unroll
     for (int off = 1; off <= 8; off <<= 1) {
 #pragma unroll
@@ -617,18 +637,55 @@ __device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [5][5] s
     }
     pcarry(l);
     const uint32_t w = threadIdx.x >> 6;
-    if (pw && w < 3) pscale(l, (3u - w) << 10, pw, 12u);  // wave-uniform
-    if ((threadIdx.x & 63u) == 0) {
+    if ((threadIdx.x & 63u) == 0 && w < nwaves) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) red[5 * w + i] = l[i];
     }
     lds_barrier();
-    if (threadIdx.x == who) {
+    if (threadIdx.x == 0) {
+        for (uint32_t k = 1; k < nwaves; ++k) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) l[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i] + (nwaves > 4 ? red[20 + i] : 0u);
+            for (int i = 0; i < 5; ++i) l[i] += red[5 * k + i];
+            if ((k & 7u) == 7u) pcarry(l);
+        }
         pcarry(l);
     }
     lds_barrier();
+}
+
+// Per-tile sums of the data waves' accumulators: the power wave's lane h gets tile h's sum (waves
+// 4h..4h+3) -- the power wave stored no data, so its publishing waits for its own stores alone.
+// pw (whole tiles): the r^(2^k) table; wave t of a tile is first scaled by r^(1024 (3 - t)) (lane
+// j's run ends 16 (255 - j) blocks before the tile's end; the in-wave part of that scaling is the
+// caller's).
+__device__ __forceinline__ void wg_sum_tiles(uint32_t l[5], uint32_t* red /* [8][5] shared */, const uint32_t* pw) {
+#pragma unroll
+    for (int off = 1; off <= 8; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] += __shfl_xor(l[i], off);
+    }
+    pcarry(l);
+    const uint32_t w = threadIdx.x >> 6, wt = w & 3u;
+    const bool data = threadIdx.x < kUData;
+    if (data && pw && wt < 3) pscale(l, (3u - wt) << 10, pw, 12u);  // wave-uniform
+    if ((threadIdx.x & 63u) == 0 && data) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) red[5 * w + i] = l[i];
+    }
+    lds_barrier();
+    const uint32_t h = threadIdx.x - kUData;  // the power wave's lane h < kUTiles takes tile h's sum
+    if (!data && h < kUTiles) {
+        const uint32_t b = 20 * h;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) l[i] = red[b + i] + red[b + 5 + i] + red[b + 10 + i] + red[b + 15 + i];
+        pcarry(l);
+    }
 }
 
 template <int MODE>
@@ -639,19 +696,27 @@ template <int MODE>
 #endif
 __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
                                                                       uint32_t* __restrict__ arrivals) {
-    __shared__ __attribute__((aligned(16))) uint8_t slab[kSegThreads * kRun];
-    __shared__ uint32_t red[25];
+    __shared__ __attribute__((aligned(16))) uint8_t slab[kUData * kRun];
+    __shared__ uint32_t red[(kUThreads / 64) * 5];
     __shared__ uint32_t pw_s[kUPow * 5];  // r^(2^k), 26-bit limbs
     __shared__ uint32_t t1_s[64 * 5];     // r^(16 i), i < 64: the in-wave part of a lane's scaling
     __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
     __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
     __shared__ uint32_t last_flag;
-    __shared__ uint32_t tab_s;  // 1: the high part of the table is in LDS (main path)
-    const bool pwv = threadIdx.x >= kSegThreads;
+    __shared__ uint32_t okr_s;  // main path: 1 once the power wave has put the one-time key in LDS
+    const bool pwv = threadIdx.x >= kUData;
     const uint32_t lane = threadIdx.x & 63u, wbase = threadIdx.x & ~63u;
-    const uint32_t j = threadIdx.x;  // data lane (< 256 in the data waves)
+    const uint32_t half = pwv ? 0u : threadIdx.x / kSegThreads;  // the workgroup's tile of this wave
+    const uint32_t j = threadIdx.x & (kSegThreads - 1);         // data lane inside its tile
+    const uint32_t wbase_t = wbase & (kSegThreads - 1);
 
-    const uint32_t rec = blockIdx.x / T, tr = blockIdx.x % T;
+    const uint32_t G = (T + kUTiles - 1) / kUTiles;  // workgroups per record
+    const uint32_t rec = blockIdx.x / G, tr = blockIdx.x % G;
+    if (threadIdx.x == 0) {
+        last_flag = 0;  // read after the publish barrier
+        okr_s = 0;
+    }
+    lds_barrier();  // the nine waves start together: this costs little and orders the resets
     if (threadIdx.x == 0) SEG_STAMP(0);
 #ifdef ENET_SEG_PROBE_TRACE
     if (threadIdx.x == 0)  // where the workgroup runs: HW_ID (cu, sh, se) and XCC_ID
@@ -696,6 +761,10 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
     // ---- the power wave: the one-time key into LDS before barrier A; then (while the data waves
     // run the tile) the table r^(2^k), k < top, and r^R before barrier B
     if (pwv) {
+        // the power wave's chain gates every tile (the key, then the table before barrier B); the
+        // issue arbiter favours older waves, and this youngest wave shared its SIMD with two data
+        // waves' keystream: without a raised priority each of its steps took ~1 us
+        __builtin_amdgcn_s_setprio(3);
         uint32_t otk[16];
 #ifdef ENET_SEG_PROBE_NO_OTK
         for (int i = 0; i < 16; ++i) otk[i] = R.k[i & 7];
@@ -705,14 +774,13 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         if (lane == 0) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) ok_s[i] = otk[i];
-            tab_s = 0;
         }
+        __hip_atomic_store(&okr_s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // The power wave's table, in two parts.  Low (before barrier B; what the tile's own scaling
-    // reads): r^(2^k), k <= 12, and in lane i r^(16 i) -- the product of r^(2^(4+b)) over the bits b
-    // of i, taken from the running square as it passes (a second chain beside the squarings).
-    // High (main path: after barrier B, while the data waves publish; read only by the record's
-    // last arriver, which waits for tab_s): r^(2^k), 13 <= k < top, and r^R.
+    // The power wave's table, built while the data waves run their tile (main path: right after
+    // the one-time key; barrier B publishes it).  Low (what a tile's own scaling reads): r^(2^k),
+    // k <= 12, and in lane i r^(16 i), the product of r^(2^(4+b)) over the bits b of i.  High (read
+    // only by the record's last arriver): r^(2^k), 13 <= k < top, and r^R.
     uint32_t px[5];  // the power wave's running square
     auto put = [&](uint32_t k) {
         if (lane == 0) {
@@ -725,18 +793,23 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         return;
 #endif
         pclamp(px, ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
-        uint32_t y[5] = {1, 0, 0, 0, 0};
-#pragma unroll
-        for (uint32_t k = 0; k < 13; ++k) {
+        // one chain at a time (few registers: this runs where the tile's key state is live).  The
+        // power wave shares a SIMD with two data waves, so every step here is slow: only what a
+        // tile's own scaling needs (k <= 11, and r^(16 i)) comes before barrier B
+#pragma unroll 1
+        for (uint32_t k = 0; k < 12; ++k) {
             put(k);
-            if (k >= 4 && k < 10) {
-                uint32_t m[5];
-                const bool on = (lane >> (k - 4)) & 1u;
+            psquare(px);
+        }
+        ENET_WAVE_LDS_SYNC();
+        uint32_t y[5] = {1, 0, 0, 0, 0};
+#pragma unroll 1
+        for (uint32_t b = 0; b < 6; ++b) {
+            uint32_t m[5];
+            const bool on = (lane >> b) & 1u;
 #pragma unroll
-                for (int i = 0; i < 5; ++i) m[i] = on ? px[i] : (i == 0 ? 1u : 0u);
-                pmul_by(y, m);
-            }
-            pmul_by(px, px);
+            for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (4 + b) + i] : (i == 0 ? 1u : 0u);
+            pmul_by(y, m);
         }
 #pragma unroll
         for (int i = 0; i < 5; ++i) t1_s[5 * lane + i] = y[i];
@@ -745,9 +818,9 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
 #ifdef ENET_SEG_PROBE_NO_TABLE
         return;
 #endif
-        for (uint32_t k = 13; k < top; ++k) {
+        for (uint32_t k = 12; k < top; ++k) {
             put(k);
-            pmul_by(px, px);
+            psquare(px);
         }
         if (nw_t) {  // R = K - (na + 4096 nw) <= 4097
             uint32_t y[5] = {1, 0, 0, 0, 0};
@@ -760,6 +833,10 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         }
     };
 
+    if (pwv && as_hinted) {  // while the data waves run their tiles
+        power_low();
+        power_high();
+    }
     uint32_t hf[5] = {0, 0, 0, 0, 0};  // the record's Poly1305 sum (thread 0), normalised at K
     PolyR32 PR{};
     if (!as_hinted) {
@@ -779,7 +856,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
             uint32_t l[5] = {0, 0, 0, 0, 0};
             const bool last_tile = tb1 == nb;
             const uint32_t tile_end = na + min(4u * tb1, nct) + (last_tile ? 1u : 0u);
-            if (!pwv) {
+            if (!pwv && half == 0) {
                 if (v == 0 && j == 0) {
                     const uint8_t* ap = p.aad + aoff;
                     for (uint32_t s2 = 0; s2 < na; ++s2) {
@@ -818,13 +895,13 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                 h32_to_limbs(h, l);
             }
             if (v == 0) __syncthreads();  // barrier B: the table in LDS
-            if (!pwv) {
+            if (!pwv && half == 0) {
                 const bool has_last = (c1 == nb && c1 > c0) || (nb == 0 && j == 0);
                 const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
                 if (c1 > c0 || (v == 0 && j == 0)) pscale(l, tile_end - lane_end, pw_s, 13u);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wg_sum5(l, red);
+            wg_sum5(l, red, kSegThreads / 64);
             if (threadIdx.x == 0) {  // H = H r^(tile_end - prev_end) + P_v
                 pscale(hf, tile_end - prev_end, pw_s, 13u);
 #pragma unroll
@@ -834,15 +911,18 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
             prev_end = tile_end;
         }
     } else {
-        const uint32_t tt = tr;  // tile index inside the record
+        const uint32_t tt = kUTiles * tr + half;  // tile index inside the record (the power wave: the first)
+        const bool tile_ok = tt < T;              // the record's last workgroup may hold one tile only
         const uint32_t tb0 = tt * kTileBlocks;
         const uint32_t tb1 = min(tb0 + kTileBlocks, nb);
         const uint32_t c0 = min(tb0 + kSegBPL * j, tb1), c1 = min(c0 + kSegBPL, tb1);
-        const bool whole = (uint64_t)(tb0 + kTileBlocks) * 64ull <= L;  // uniform over the workgroup
+        // uniform over the tile's waves (an absent tile: the per-block path over no blocks)
+        const bool whole = tile_ok && (uint64_t)(tb0 + kTileBlocks) * 64ull <= L;
         const bool first_iter = true;
         uint32_t h[5] = {0, 0, 0, 0, 0};
-        auto barrier_a = [&]() {  // r / s in LDS
-            lds_barrier();
+        auto barrier_a = [&]() {  // r / s in LDS: wait for the power wave's flag (no barrier)
+            while (__hip_atomic_load(&okr_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+                __builtin_amdgcn_s_sleep(1);
             if (threadIdx.x == 0) SEG_STAMP(1);
             PR = polyr32_make(ok_s[0], ok_s[1], ok_s[2], ok_s[3]);
         };
@@ -878,7 +958,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const uint32_t o = 8u * i + (lane >> 3);
-                    offs[i] = 64u * kSegBPL * (wbase + o) + 16u * (kk ^ slab_sw(o));
+                    offs[i] = 64u * kSegBPL * (wbase_t + o) + 16u * (kk ^ slab_sw(o));
                 }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -890,6 +970,9 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
             for (int st = 0; st < 2; ++st) {
                 uint32_t w2[32], ka[16], kb[16];
                 if (!pwv) {
+                    // the keystream first: it needs no data, so it runs under the loads' latency
+                    const uint32_t cb = 1u + c0 + 2u * st;  // RFC 8439 data counter from 1
+                    chacha_block2(R, cb, cb + 1u, ka, kb);
                     ENET_WAVE_LDS_SYNC();
 #pragma unroll
                     for (int i = 0; i < 8; ++i)
@@ -909,8 +992,6 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                         }
                         asm volatile("" : "+v"(R.k[0])::"memory");
                     }
-                    const uint32_t cb = 1u + c0 + 2u * st;  // RFC 8439 data counter from 1
-                    chacha_block2(R, cb, cb + 1u, ka, kb);
                 }
                 if (st == 0 && first_iter) {
                     barrier_a();
@@ -1003,19 +1084,12 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         // the power wave skipped the tile's body: it builds the table here, where no tile data
         // is live (inside the body its registers would count against every wave)
         if (threadIdx.x == 0) SEG_STAMP(2);
-        if (pwv) power_low();
-        if (threadIdx.x == kSegThreads) SEG_STAMP(3);
+        if (threadIdx.x == kUData) SEG_STAMP(3);
 #ifndef ENET_SEG_PROBE_NO_SYNC
         lds_barrier();  // barrier B: the table's low part in LDS
 #endif
         if (threadIdx.x == 0) SEG_STAMP(4);
-        if (pwv) {
-            // the high part, then the power wave leaves: the barriers below wait on the data waves
-            // alone (s_barrier counts the workgroup's surviving waves)
-            power_high();
-            __hip_atomic_store(&tab_s, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
-        }
+
 #ifndef ENET_SEG_PROBE_NO_SCALE
         if (!pwv) {
             const uint32_t lane_end = na + min(4u * c1, nct) + (has_last ? 1u : 0u);
@@ -1040,15 +1114,17 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         // open: every wave drains its write-through plaintext before the arrival (the last arriver
         // may zero the record)
         if (MODE == MODE_OPEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wg_sum5(l, red, 0, whole ? pw_s : nullptr, 4);
-        // main path: publish, take a ticket; the last tile of the record to arrive finishes it
-        uint32_t* part = p.partials + 8ull * blockIdx.x;
+        wg_sum_tiles(l, red, whole ? pw_s : nullptr);
+        // main path: each tile publishes (the power wave's lane h for tile h), takes a ticket; the
+        // record's last tile to arrive finishes it
         uint32_t* ctr = arrivals + (size_t)kUArrStride * rec;  // [0] top, [32 (1 + g)] group g
-        if (threadIdx.x == 0) {
+        const uint32_t tp = kUTiles * tr + lane;  // the power wave lane's tile
+        if (pwv && lane < kUTiles && tp < T) {
+            uint32_t* part = p.partials + 8ull * ((size_t)rec * T + tp);
 #pragma unroll
             for (int i = 0; i < 5; ++i) __hip_atomic_store(part + i, l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t ng = min(T, kUGroups), g = tt % ng, members = (T - g + ng - 1) / ng;
+            const uint32_t ng = min(T, kUGroups), g = tp % ng, members = (T - g + ng - 1) / ng;
             uint32_t* gc = ctr + 32 * (1 + g);
             const uint32_t prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint32_t lf = 0;
@@ -1057,8 +1133,8 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                 const uint32_t top_prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 lf = top_prev + 1 == ng ? 1u : 0u;
             }
-            last_flag = lf;
-            SEG_STAMP(5);
+            if (lf) last_flag = 1u;
+            if (lane == 0) SEG_STAMP(5);
         }
         lds_barrier();
 #ifdef ENET_SEG_PROBE_NO_TAIL
@@ -1066,6 +1142,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         return;
 #endif
         if (!last_flag) return;  // uniform over the workgroup
+        if (threadIdx.x >= kSegThreads) return;  // the combine runs on the first tile's four waves
         const uint32_t* parts = p.partials + 8ull * ((size_t)rec * T);
         uint32_t vl[5] = {0, 0, 0, 0, 0};  // the last tile's partial, normalised at K: loaded first
         if (threadIdx.x == 0) {
@@ -1104,9 +1181,6 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                     for (int i = 0; i < 5; ++i) acc[i] += cur[i];
                     pcarry(acc);
                 }
-                // the high part of the table (the power wave's, after barrier B)
-                while (__hip_atomic_load(&tab_s, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-                    __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                 for (uint32_t d = 1, lev = 0; d < 64; d <<= 1, ++lev) {
                     uint32_t o[5], x[5], mm[5];
@@ -1219,7 +1293,7 @@ extern "C" __attribute__((visibility("default"))) int enet_probe_trace_read(uint
 
 hipError_t launch_seg_uniform_aead(const SegParams& p, uint64_t L, uint32_t* arrivals, hipStream_t s) {
     const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
-    const uint64_t blocks = (uint64_t)p.n * T;
+    const uint64_t blocks = (uint64_t)p.n * ((T + kUTiles - 1) / kUTiles);
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7FFFFFFFull || T > 0xFFFFFFFFull) return hipErrorInvalidValue;
     switch (p.mode) {

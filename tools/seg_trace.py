@@ -19,7 +19,7 @@ def main() -> None:
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream(dev)
     L = 32 << 20
-    T = L >> 16
+    T = (L >> 16 + 1) // 2  # workgroups: two 64 KiB tiles each (segments.hip kUTiles)
     g = torch.Generator(device=dev).manual_seed(5)
     pt = torch.randint(0, 256, (L,), dtype=torch.uint8, device=dev, generator=g)
     keys = torch.randint(0, 256, (32,), dtype=torch.uint8, device=dev, generator=g)
