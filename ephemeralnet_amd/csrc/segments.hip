@@ -583,12 +583,11 @@ __global__ __launch_bounds__(kSegThreads) void seg_uniform_xor_kernel(SegParams 
 //     by each record's last arriver;
 //   * a record whose real length differs from the hint is run whole by its tile-0 workgroup, tile
 //     after tile, its partials combined in that workgroup (a wrong hint costs speed, never bytes).
-// Two tiles per workgroup (eight data waves) + the power wave: nine waves of 152 VGPRs fit a CU
-// (three per SIMD), so a 32 MiB record's 512 tiles are all resident at once.  (One tile per
-// five-wave workgroup ran in two rounds: a second such workgroup did not fit beside the first.)
-constexpr uint32_t kUTiles = 2;
-constexpr uint32_t kUData = kSegThreads * kUTiles;  // data threads
-constexpr uint32_t kUThreads = kUData + 64;         // + the power wave
+// TPW tiles per workgroup (4 TPW data waves) + the power wave.  Past one tile per CU, two tiles
+// per nine-wave workgroup (three waves of ~166 VGPRs per SIMD fit) keep a 32 MiB record's 512
+// tiles resident at once; one tile per five-wave workgroup ran in two rounds there (a second such
+// workgroup did not fit beside the first).  Up to one tile per CU, one tile per workgroup spreads
+// the tiles over the most CUs.
 #ifdef ENET_SEG_PROBE_TRACE
 // timing probe: per-workgroup wall-clock stamps (100 MHz) at the phase boundaries, read back by
 // tools/seg_trace.py through enet_probe_trace_read (hand-built libraries only)
@@ -658,7 +657,9 @@ __device__ __forceinline__ void wg_sum5(uint32_t l[5], uint32_t* red /* [waves][
 // pw (whole tiles): the r^(2^k) table; wave t of a tile is first scaled by r^(1024 (3 - t)) (lane
 // j's run ends 16 (255 - j) blocks before the tile's end; the in-wave part of that scaling is the
 // caller's).
-__device__ __forceinline__ void wg_sum_tiles(uint32_t l[5], uint32_t* red /* [8][5] shared */, const uint32_t* pw) {
+template <int TPW>
+__device__ __forceinline__ void wg_sum_tiles(uint32_t l[5], uint32_t* red /* [4 TPW][5] shared */, const uint32_t* pw) {
+    constexpr uint32_t kUTiles = TPW, kUData = kSegThreads * TPW;
 #pragma unroll
     for (int off = 1; off <= 8; off <<= 1) {
 #pragma unroll
@@ -688,18 +689,17 @@ __device__ __forceinline__ void wg_sum_tiles(uint32_t l[5], uint32_t* red /* [8]
     }
 }
 
-template <int MODE>
-#ifdef ENET_SEG_PROBE_LB4
-#define ENET_UAEAD_BOUNDS __launch_bounds__(kUThreads, 4)
-#else
-#define ENET_UAEAD_BOUNDS __launch_bounds__(kUThreads)
-#endif
-__global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
-                                                                      uint32_t* __restrict__ arrivals) {
+template <int MODE, int TPW>
+__global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kernel(SegParams p, uint64_t Lh, uint32_t T,
+                                                                                 uint32_t* __restrict__ arrivals) {
+    constexpr uint32_t kUTiles = TPW;                    // tiles per workgroup
+    constexpr uint32_t kUData = kSegThreads * kUTiles;  // data threads
+    constexpr uint32_t kUThreads = kUData + 64;         // + the power wave
     __shared__ __attribute__((aligned(16))) uint8_t slab[kUData * kRun];
     __shared__ uint32_t red[(kUThreads / 64) * 5];
     __shared__ uint32_t pw_s[kUPow * 5];  // r^(2^k), 26-bit limbs
     __shared__ uint32_t t1_s[64 * 5];     // r^(16 i), i < 64: the in-wave part of a lane's scaling
+    __shared__ uint32_t t2_s[64 * 5];     // r^(4096 q i), i < 64: the same for the combine's lanes
     __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
     __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
     __shared__ uint32_t last_flag;
@@ -830,6 +830,18 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
 #pragma unroll
                 for (int i = 0; i < 5; ++i) rr_s[i] = y[i];
             }
+            // lane i: r^(4096 q i), q = 2^lq, from entries 12 + lq .. 12 + lq + 5
+            uint32_t z[5] = {1, 0, 0, 0, 0};
+#pragma unroll 1
+            for (uint32_t b = 0; b < 6; ++b) {
+                uint32_t m[5];
+                const bool on = (lane >> b) & 1u;
+#pragma unroll
+                for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (12 + lq + b) + i] : (i == 0 ? 1u : 0u);
+                pmul_by(z, m);
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) t2_s[5 * lane + i] = z[i];
         }
     };
 
@@ -1114,7 +1126,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
         // open: every wave drains its write-through plaintext before the arrival (the last arriver
         // may zero the record)
         if (MODE == MODE_OPEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wg_sum_tiles(l, red, whole ? pw_s : nullptr);
+        wg_sum_tiles<TPW>(l, red, whole ? pw_s : nullptr);
         // main path: each tile publishes (the power wave's lane h for tile h), takes a ticket; the
         // record's last tile to arrive finishes it
         uint32_t* ctr = arrivals + (size_t)kUArrStride * rec;  // [0] top, [32 (1 + g)] group g
@@ -1124,6 +1136,13 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
 #pragma unroll
             for (int i = 0; i < 5; ++i) __hip_atomic_store(part + i, l[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef ENET_SEG_PROBE_ONECTR
+            uint32_t lf = 0;
+            if (lane == 0) {  // one add per workgroup at one counter per record
+                const uint32_t nw = min(kUTiles, T - kUTiles * tr);
+                lf = __hip_atomic_fetch_add(ctr, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + nw == T ? 1u : 0u;
+            }
+#else
             const uint32_t ng = min(T, kUGroups), g = tp % ng, members = (T - g + ng - 1) / ng;
             uint32_t* gc = ctr + 32 * (1 + g);
             const uint32_t prev = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1133,6 +1152,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                 const uint32_t top_prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 lf = top_prev + 1 == ng ? 1u : 0u;
             }
+#endif
             if (lf) last_flag = 1u;
             if (lane == 0) SEG_STAMP(5);
         }
@@ -1181,44 +1201,43 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
                     for (int i = 0; i < 5; ++i) acc[i] += cur[i];
                     pcarry(acc);
                 }
+                // lane (of 64) l's tiles end 64 - 1 - l lane-runs of q tiles before its wave's last
+                // one: r^(4096 q (63 - l)) from the power wave's T2, then plain sums in the wave
+                {
+                    uint32_t mm[5];
 #pragma unroll
-                for (uint32_t d = 1, lev = 0; d < 64; d <<= 1, ++lev) {
-                    uint32_t o[5], x[5], mm[5];
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) o[i] = __shfl_xor(acc[i], (int)d);
-                    const bool left = (lane & d) == 0u;  // the earlier tiles
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) {
-                        x[i] = left ? acc[i] : o[i];
-                        o[i] = left ? o[i] : acc[i];
-                    }
-                    pw_at(12 + lq + lev, mm);
-                    pmul_by(x, mm);
-#pragma unroll
-                    for (int i = 0; i < 5; ++i) acc[i] = x[i] + o[i];
-                    pcarry(acc);
+                    for (int i = 0; i < 5; ++i) mm[i] = t2_s[5 * (63u - lane) + i];
+                    pmul_by(acc, mm);
                 }
+#pragma unroll
+                for (int off = 1; off <= 8; off <<= 1) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) acc[i] += __shfl_xor(acc[i], off);
+                }
+                pcarry(acc);
+#pragma unroll
+                for (int off = 16; off <= 32; off <<= 1) {
+#pragma unroll
+                    for (int i = 0; i < 5; ++i) acc[i] += __shfl_xor(acc[i], off);
+                }
+                pcarry(acc);
+                // wave w's runs end 64 (3 - w) lane-runs before the last wave's: entries 12+lq+6, +7
+                const uint32_t w = threadIdx.x >> 6;
+                if ((3u - w) & 1u) pmul_by(acc, pw_s + 5 * (12 + lq + 6));  // wave-uniform
+                if ((3u - w) & 2u) pmul_by(acc, pw_s + 5 * (12 + lq + 7));
                 if (lane == 0) {
 #pragma unroll
-                    for (int i = 0; i < 5; ++i) red[5 * (threadIdx.x >> 6) + i] = acc[i];
+                    for (int i = 0; i < 5; ++i) red[5 * w + i] = acc[i];
                 }
             }
-            __syncthreads();
+            lds_barrier();
             if (threadIdx.x == 0) {
-                uint32_t A[5], B[5], m6[5], m7[5], rr[5];
-                pw_at(12 + lq + 6, m6);
-                pw_at(12 + lq + 7, m7);
+                uint32_t rr[5];
 #pragma unroll
-                for (int i = 0; i < 5; ++i) { A[i] = red[i]; B[i] = red[10 + i]; }
-                pmul_by(A, m6);
-                pmul_by(B, m6);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) { A[i] += red[5 + i]; B[i] += red[15 + i]; }
-                pcarry(A);
-                pcarry(B);
-                pmul_by(A, m7);
-#pragma unroll
-                for (int i = 0; i < 5; ++i) { acc[i] = A[i] + B[i]; rr[i] = rr_s[i]; }
+                for (int i = 0; i < 5; ++i) {
+                    acc[i] = red[i] + red[5 + i] + red[10 + i] + red[15 + i];
+                    rr[i] = rr_s[i];
+                }
                 pcarry(acc);
                 pmul_by(acc, rr);
             }
@@ -1251,7 +1270,7 @@ __global__ ENET_UAEAD_BOUNDS void seg_uniform_aead_kernel(SegParams p, uint64_t 
 #endif
     if (MODE == MODE_OPEN) {
         __syncthreads();
-        const uint32_t zt = as_hinted ? kSegThreads : kUThreads;  // the main path's power wave has left
+        const uint32_t zt = as_hinted ? kSegThreads : kUThreads;  // the main path's combine: 4 waves
         if (last_flag && threadIdx.x < zt) {
             for (uint64_t b = 16ull * threadIdx.x; b < L; b += 16ull * zt) {
                 const uint32_t nbytes = (uint32_t)min<uint64_t>(16, L - b);
@@ -1293,17 +1312,22 @@ extern "C" __attribute__((visibility("default"))) int enet_probe_trace_read(uint
 
 hipError_t launch_seg_uniform_aead(const SegParams& p, uint64_t L, uint32_t* arrivals, hipStream_t s) {
     const uint64_t T = (L + kTileBytes - 1) / kTileBytes;
-    const uint64_t blocks = (uint64_t)p.n * ((T + kUTiles - 1) / kUTiles);
-    if (blocks == 0) return hipSuccess;
-    if (blocks > 0x7FFFFFFFull || T > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if ((uint64_t)p.n * T == 0) return hipSuccess;
+    if (T > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const bool two = (uint64_t)p.n * T > (uint64_t)(cus > 0 ? cus : 256);  // tiles per workgroup
+    const uint64_t blocks = (uint64_t)p.n * (two ? (T + 1) / 2 : T);
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const dim3 g((uint32_t)blocks), b1(kSegThreads + 64), b2(2 * kSegThreads + 64);
     switch (p.mode) {
         case MODE_SEAL:
-            hipLaunchKernelGGL(seg_uniform_aead_kernel<MODE_SEAL>, dim3((uint32_t)blocks), dim3(kUThreads), 0, s, p, L,
-                               (uint32_t)T, arrivals);
+            if (two) hipLaunchKernelGGL((seg_uniform_aead_kernel<MODE_SEAL, 2>), g, b2, 0, s, p, L, (uint32_t)T, arrivals);
+            else hipLaunchKernelGGL((seg_uniform_aead_kernel<MODE_SEAL, 1>), g, b1, 0, s, p, L, (uint32_t)T, arrivals);
             break;
         case MODE_OPEN:
-            hipLaunchKernelGGL(seg_uniform_aead_kernel<MODE_OPEN>, dim3((uint32_t)blocks), dim3(kUThreads), 0, s, p, L,
-                               (uint32_t)T, arrivals);
+            if (two) hipLaunchKernelGGL((seg_uniform_aead_kernel<MODE_OPEN, 2>), g, b2, 0, s, p, L, (uint32_t)T, arrivals);
+            else hipLaunchKernelGGL((seg_uniform_aead_kernel<MODE_OPEN, 1>), g, b1, 0, s, p, L, (uint32_t)T, arrivals);
             break;
         default: return hipErrorInvalidValue;
     }

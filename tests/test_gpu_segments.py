@@ -236,8 +236,17 @@ def test_seg_uniform_xor_one_launch_and_lying_hints(enet, lens):
             assert oh[offs[i]:offs[i + 1]] == want, f"record {i} (len {lens[i]}, in place {inplace})"
 
 
+H53 = 52 * 65536 + 100  # 53 tiles, the last one ragged
+
+
 @pytest.mark.parametrize("with_aad", [False, True])
-@pytest.mark.parametrize("lens", [[300 << 10] * 5, [300 << 10, 100, (600 << 10) + 7, 0, 300 << 10, 65536 + 1, 4095]])
+@pytest.mark.parametrize("lens", [
+    [300 << 10] * 5,
+    [300 << 10, 100, (600 << 10) + 7, 0, 300 << 10, 65536 + 1, 4095],
+    # > 256 tiles: two tiles per workgroup, an odd tile count (the last workgroup holds one)
+    [H53] * 6,
+    [H53, 100, H53, 0, H53 - 1, H53, H53, H53 + 70000],
+], ids=["5x300K", "300K_lying", "6x53tiles", "53tiles_lying"])
 def test_seg_uniform_aead_one_launch_lying_hints_tamper(enet, lens, with_aad):
     """RFC 8439 seal / open over a batch the hints call uniform (n x 300 KiB): one launch -- each
     record's last tile to arrive combines the partials and, on open, zeroes a failed record itself
@@ -246,11 +255,13 @@ def test_seg_uniform_aead_one_launch_lying_hints_tamper(enet, lens, with_aad):
     oracle (tags pinned by RFC 8439 / OpenSSL through the oracle's golden checks), every record
     opens; then a flipped tag on an as-hinted record, a flipped ciphertext byte in another and in
     a fallback record: those three fail and are zeroed, the rest open.  Runs twice: the per-stream
-    arrival counters must be back at zero for the second launch."""
+    arrival counters must be back at zero for the second launch.  The last two shapes have more
+    tiles than the chip has CUs (two tiles per workgroup) and 53 tiles per record."""
     import torch
     n = len(lens)
+    H = max(set(lens), key=lens.count)  # the hinted length
     b, items, keys, nonces = make(enet, lens, 9600 + len(lens) + (7 if with_aad else 0))
-    hint = dict(total_bytes_hint=n * (300 << 10), max_len_hint=300 << 10)
+    hint = dict(total_bytes_hint=n * H, max_len_hint=H)
     aads = [splitmix_bytes(9900 + i, (i * 37) % 90) for i in range(n)] if with_aad else None
     aad = aad_off = None
     if with_aad:
@@ -283,8 +294,8 @@ def test_seg_uniform_aead_one_launch_lying_hints_tamper(enet, lens, with_aad):
         for i in range(n):
             assert bh[offs[i]:offs[i + 1]] == items[i], f"plaintext {i} (rep {rep})"
     # tamper
-    hinted = [i for i in range(n) if lens[i] == 300 << 10]
-    fallback = [i for i in range(n) if lens[i] != 300 << 10 and lens[i] > 0]
+    hinted = [i for i in range(n) if lens[i] == H]
+    fallback = [i for i in range(n) if lens[i] != H and lens[i] > 0]
     bad_tags = tags.clone()
     bad_tags[16 * hinted[0] + 3] ^= 0x40
     ct2 = ct.clone()
