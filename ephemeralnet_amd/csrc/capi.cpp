@@ -205,15 +205,19 @@ struct SegRun {
     const uint8_t* claimed = nullptr;
 };
 
-// Per-stream arrival counters of the one-launch AEAD path (segments.hip seg_uniform_aead_kernel):
-// zeroed when allocated, reset by each record's last arriver, so they are zero whenever a launch
-// on that stream starts (launches on one stream run in order).  Grown on demand, stream-ordered.
+// Per-stream state of the one-launch AEAD path (segments.hip seg_uniform_aead_kernel): arrival
+// counters, zeroed when allocated and reset by each record's last arriver, so they are zero
+// whenever a launch on that stream starts (launches on one stream run in order); and the tiles'
+// partials.  Grown on demand, stream-ordered; otherwise reused, so a launch makes no allocation
+// (a stream-ordered allocate / free pair per call cost ~4 us of gap between launches).
 struct Arrivals {
     uint32_t* ptr = nullptr;
     uint32_t cap = 0;
+    void* part = nullptr;
+    size_t part_cap = 0;
 };
 
-int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out) {
+int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out, size_t part_bytes = 0, void** part_out = nullptr) {
     static std::mutex mu;
     static std::vector<std::pair<std::pair<int, hipStream_t>, Arrivals>> table;
     int dev = 0;
@@ -237,6 +241,17 @@ int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out) {
         a->ptr = static_cast<uint32_t*>(mem);
         a->cap = cap;
     }
+    if (part_out && a->part_cap < part_bytes) {
+        hipMemPool_t pool = seg_pool();
+        if (!pool) return fail(ENET_EHIP, "aead tiles: no memory pool for the current device");
+        const size_t cap = std::max<size_t>(part_bytes, 64u << 10);
+        void* mem = nullptr;
+        if (hipError_t e = hipMallocFromPoolAsync(&mem, cap, pool, st)) return hip_status(e, "aead tiles: scratch");
+        if (a->part) (void)hipFreeAsync(a->part, st);
+        a->part = mem;
+        a->part_cap = cap;
+    }
+    if (part_out) *part_out = a->part;
     out = a->ptr;
     return ENET_OK;
 }
@@ -249,12 +264,8 @@ int run_uniform_aead(int mode, const enet_records* r, const enet::RecParams& p, 
     uint32_t* arr = nullptr;
     const uint64_t words = (uint64_t)r->count * enet::seg_uniform_arrival_words();
     if (words > UINT32_MAX) return fail(ENET_EINVAL, "aead tiles: too many records for one launch");
-    if (int e = arrivals_for(st, (uint32_t)words, arr)) return e;
-    hipMemPool_t pool = seg_pool();
-    if (!pool) return fail(ENET_EHIP, "aead tiles: no memory pool for the current device");
-    const size_t bytes = (size_t)tiles * 32;
     void* mem = nullptr;
-    if (hipError_t e = hipMallocFromPoolAsync(&mem, bytes, pool, st)) return hip_status(e, "aead tiles: scratch");
+    if (int e = arrivals_for(st, (uint32_t)words, arr, (size_t)tiles * 32, &mem)) return e;
     enet::SegParams q{};
     q.mode = mode;
     q.n = r->count;
@@ -272,9 +283,7 @@ int run_uniform_aead(int mode, const enet_records* r, const enet::RecParams& p, 
     q.ok = p.ok;
     q.partials = static_cast<uint32_t*>(mem);
     g_seg_batches.fetch_add(1, std::memory_order_relaxed);
-    const int rc = hip_status(enet::launch_seg_uniform_aead(q, L, arr, st), what);
-    (void)hipFreeAsync(mem, st);
-    return rc;
+    return hip_status(enet::launch_seg_uniform_aead(q, L, arr, st), what);
 }
 
 // Plan + tile kernels for the batch's long records; sr.claimed marks them for the record engine.
