@@ -698,7 +698,7 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
     __shared__ __attribute__((aligned(16))) uint8_t slab[kUData * kRun];
     __shared__ uint32_t red[(kUThreads / 64) * 5];
     __shared__ uint32_t pw_s[kUPow * 5];  // r^(2^k), 26-bit limbs
-    __shared__ uint32_t t1_s[64 * 5];     // r^(16 i), i < 64: the in-wave part of a lane's scaling
+    __shared__ uint32_t t1_s[4 * 64 * 5];  // [m][i]: r^(16 i + 1024 m), a tile lane's scaling
     __shared__ uint32_t t2_s[64 * 5];     // r^(4096 q i), i < 64: the same for the combine's lanes
     __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
     __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
@@ -811,8 +811,13 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
             for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (4 + b) + i] : (i == 0 ? 1u : 0u);
             pmul_by(y, m);
         }
+        // then times r^1024 per wave of the tile: entry [m][i] = r^(16 i + 1024 m)
+#pragma unroll 1
+        for (uint32_t m = 0; m < 4; ++m) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) t1_s[5 * lane + i] = y[i];
+            for (int i = 0; i < 5; ++i) t1_s[5 * (64 * m + lane) + i] = y[i];
+            if (m < 3) pmul_by(y, pw_s + 5 * 10);
+        }
     };
     auto power_high = [&]() {
 #ifdef ENET_SEG_PROBE_NO_TABLE
@@ -1108,10 +1113,11 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
             const uint32_t e = tile_end - lane_end;
             if (whole) {
                 // e = 16 (255 - j) (+1 in the record's last tile for lanes before the length
-                // block): r^(16 (63 - lane)) here, r^(1024 (3 - wave)) on the wave's sum
+                // block) = 16 (63 - lane) + 1024 (3 - wave of the tile): one table entry
                 uint32_t m[5];
+                const uint32_t wt = (threadIdx.x >> 6) & 3u;
 #pragma unroll
-                for (int i = 0; i < 5; ++i) m[i] = t1_s[5 * (63u - lane) + i];
+                for (int i = 0; i < 5; ++i) m[i] = t1_s[5 * (64 * (3u - wt) + 63u - lane) + i];
                 pmul_by(l, m);
                 if (e != 16u * (255u - j)) {
 #pragma unroll
@@ -1126,7 +1132,7 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
         // open: every wave drains its write-through plaintext before the arrival (the last arriver
         // may zero the record)
         if (MODE == MODE_OPEN) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wg_sum_tiles<TPW>(l, red, whole ? pw_s : nullptr);
+        wg_sum_tiles<TPW>(l, red, nullptr);  // whole tiles: the wave factor is in the lane's entry
         // main path: each tile publishes (the power wave's lane h for tile h), takes a ticket; the
         // record's last tile to arrive finishes it
         uint32_t* ctr = arrivals + (size_t)kUArrStride * rec;  // [0] top, [32 (1 + g)] group g
