@@ -699,7 +699,7 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
     __shared__ uint32_t red[(kUThreads / 64) * 5];
     __shared__ uint32_t pw_s[kUPow * 5];  // r^(2^k), 26-bit limbs
     __shared__ uint32_t t1_s[4 * 64 * 5];  // [m][i]: r^(16 i + 1024 m), a tile lane's scaling
-    __shared__ uint32_t t2_s[64 * 5];     // r^(4096 q i), i < 64: the same for the combine's lanes
+    __shared__ uint32_t t2_s[4 * 64 * 5];  // [m][i]: r^(4096 q (i + 64 m)), the combine's lanes
     __shared__ uint32_t rr_s[5];          // r^R: the last tile's offset from tile nw-1's end
     __shared__ uint32_t ok_s[8];       // one-time key words: r (raw) then s
     __shared__ uint32_t last_flag;
@@ -845,8 +845,12 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
                 for (int i = 0; i < 5; ++i) m[i] = on ? pw_s[5 * (12 + lq + b) + i] : (i == 0 ? 1u : 0u);
                 pmul_by(z, m);
             }
+#pragma unroll 1
+            for (uint32_t m = 0; m < 4; ++m) {  // times r^(4096 q 64) per wave
 #pragma unroll
-            for (int i = 0; i < 5; ++i) t2_s[5 * lane + i] = z[i];
+                for (int i = 0; i < 5; ++i) t2_s[5 * (64 * m + lane) + i] = z[i];
+                if (m < 3) pmul_by(z, pw_s + 5 * (12 + lq + 6));
+            }
         }
     };
 
@@ -1207,12 +1211,14 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
                     for (int i = 0; i < 5; ++i) acc[i] += cur[i];
                     pcarry(acc);
                 }
-                // lane (of 64) l's tiles end 64 - 1 - l lane-runs of q tiles before its wave's last
-                // one: r^(4096 q (63 - l)) from the power wave's T2, then plain sums in the wave
+                // lane l of wave w: its tiles end 63 - l + 64 (3 - w) lane-runs of q tiles before
+                // the last lane's: r^(4096 q (63 - l + 64 (3 - w))), one entry of the power wave's
+                // table; then plain sums
+                const uint32_t w = threadIdx.x >> 6;
                 {
                     uint32_t mm[5];
 #pragma unroll
-                    for (int i = 0; i < 5; ++i) mm[i] = t2_s[5 * (63u - lane) + i];
+                    for (int i = 0; i < 5; ++i) mm[i] = t2_s[5 * (64 * (3u - w) + 63u - lane) + i];
                     pmul_by(acc, mm);
                 }
 #pragma unroll
@@ -1227,10 +1233,6 @@ __global__ __launch_bounds__(kSegThreads * TPW + 64) void seg_uniform_aead_kerne
                     for (int i = 0; i < 5; ++i) acc[i] += __shfl_xor(acc[i], off);
                 }
                 pcarry(acc);
-                // wave w's runs end 64 (3 - w) lane-runs before the last wave's: entries 12+lq+6, +7
-                const uint32_t w = threadIdx.x >> 6;
-                if ((3u - w) & 1u) pmul_by(acc, pw_s + 5 * (12 + lq + 6));  // wave-uniform
-                if ((3u - w) & 2u) pmul_by(acc, pw_s + 5 * (12 + lq + 7));
                 if (lane == 0) {
 #pragma unroll
                     for (int i = 0; i < 5; ++i) red[5 * w + i] = acc[i];
