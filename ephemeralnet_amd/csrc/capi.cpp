@@ -215,9 +215,12 @@ struct Arrivals {
     uint32_t cap = 0;
     void* part = nullptr;
     size_t part_cap = 0;
+    void* seg = nullptr;  // the plan + tiles path's scratch (seg_begin)
+    size_t seg_cap = 0;
 };
 
-int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out, size_t part_bytes = 0, void** part_out = nullptr) {
+int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out, size_t part_bytes = 0, void** part_out = nullptr,
+                 size_t seg_bytes = 0, void** seg_out = nullptr) {
     static std::mutex mu;
     static std::vector<std::pair<std::pair<int, hipStream_t>, Arrivals>> table;
     int dev = 0;
@@ -252,6 +255,17 @@ int arrivals_for(hipStream_t st, uint32_t n, uint32_t*& out, size_t part_bytes =
         a->part_cap = cap;
     }
     if (part_out) *part_out = a->part;
+    if (seg_out && a->seg_cap < seg_bytes) {
+        hipMemPool_t pool = seg_pool();
+        if (!pool) return fail(ENET_EHIP, "sequence-parallel scratch: no memory pool for the current device");
+        const size_t cap = std::max<size_t>(seg_bytes, 256u << 10);
+        void* mem = nullptr;
+        if (hipError_t e = hipMallocFromPoolAsync(&mem, cap, pool, st)) return hip_status(e, "sequence-parallel scratch");
+        if (a->seg) (void)hipFreeAsync(a->seg, st);
+        a->seg = mem;
+        a->seg_cap = cap;
+    }
+    if (seg_out) *seg_out = a->seg;
     out = a->ptr;
     return ENET_OK;
 }
@@ -298,13 +312,12 @@ int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long
     const uint64_t tcap = std::min<uint64_t>(total / enet::kSegTileBytes + ecap + 1, 0xFFFFFFFFull);
     const size_t o_ent = 256, o_cl = o_ent + (size_t)ecap * sizeof(enet::SegEntry),
                  o_part = (o_cl + index_n + 255) & ~size_t(255), bytes = o_part + (size_t)tcap * 32;
-    hipMemPool_t pool = seg_pool();
-    if (!pool) return fail(ENET_EHIP, "sequence-parallel scratch: no memory pool for the current device");
-    if (hipError_t e = hipMallocFromPoolAsync(&sr.mem, bytes, pool, st)) {
-        sr.mem = nullptr;
-        return hip_status(e, "sequence-parallel scratch");
-    }
-    uint8_t* base = static_cast<uint8_t*>(sr.mem);
+    // per-stream scratch, reused: one seg run per call, calls on a stream run in order, and the
+    // plan kernel initialises everything the tiles read (no allocate / free pair per call)
+    uint32_t* unused = nullptr;
+    void* mem = nullptr;
+    if (int e = arrivals_for(st, 0, unused, 0, nullptr, bytes, &mem)) return e;
+    uint8_t* base = static_cast<uint8_t*>(mem);
     enet::SegParams q{};
     q.mode = mode;
     q.n = n;
@@ -338,8 +351,8 @@ int seg_begin(int mode, const enet_records* r, enet::RecParams& p, uint64_t long
 }
 
 void seg_end(SegRun& sr, hipStream_t st) {
-    if (sr.mem) (void)hipFreeAsync(sr.mem, st);
-    sr.mem = nullptr;
+    (void)sr;
+    (void)st;
 }
 
 // The record engine over the batch, with the long records on the tiles first when seg_wanted
