@@ -479,6 +479,11 @@ __device__ __forceinline__ void xor_tile(const uint8_t* src, uint8_t* dst, uint6
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
+            const uint32_t cb = ctr0 + c0 + 2u * st;  // u32 wrap (ChaCha20.cpp:110)
+            uint32_t ka[16], kb[16];
+#ifndef ENET_SEG_PROBE_XOR_OLD
+            chacha_block2(R, cb, cb + 1u, ka, kb);  // the keystream first, under the loads' latency
+#endif
             ENET_WAVE_LDS_SYNC();
 #pragma unroll
             for (int i = 0; i < 8; ++i)
@@ -498,9 +503,9 @@ __device__ __forceinline__ void xor_tile(const uint8_t* src, uint8_t* dst, uint6
                     pf[4 * i] = v.x; pf[4 * i + 1] = v.y; pf[4 * i + 2] = v.z; pf[4 * i + 3] = v.w;
                 }
             }
-            const uint32_t cb = ctr0 + c0 + 2u * st;  // u32 wrap (ChaCha20.cpp:110)
-            uint32_t ka[16], kb[16];
+#ifdef ENET_SEG_PROBE_XOR_OLD
             chacha_block2(R, cb, cb + 1u, ka, kb);
+#endif
 #pragma unroll
             for (int i = 0; i < 16; ++i) { w2[i] ^= ka[i]; w2[16 + i] ^= kb[i]; }
             ENET_WAVE_LDS_SYNC();
