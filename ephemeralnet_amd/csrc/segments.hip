@@ -605,7 +605,11 @@ constexpr uint32_t kUPow = 44;                      // LDS table entries r^(2^k)
 // Arrival counters per record: a top counter and kUGroups group counters, each on its own 128-byte
 // line.  Tile t arrives at group t mod kUGroups; a group's last arriver arrives at the top counter.
 // (One counter per record took all of a 32 MiB record's 512 arrivals at one address.)
+#ifdef ENET_SEG_PROBE_GROUPS
+constexpr uint32_t kUGroups = ENET_SEG_PROBE_GROUPS;  // timing probe
+#else
 constexpr uint32_t kUGroups = 16;
+#endif
 constexpr uint32_t kUArrStride = 32 * (1 + kUGroups);
 
 typedef uint32_t enet_v4u __attribute__((ext_vector_type(4)));
